@@ -1,0 +1,222 @@
+// bvh.cpp -- per-mesh BLAS for the ACCEL_BVH intersect path.
+//
+// Binned-SAH 2-wide BVH in model space.  Boxes bound the region the
+// reference's triangle test (Renderer.cpp:174-215) can accept -- the
+// triangle grown by its u/v tolerances (EPSILON = 0.005 in barycentric
+// units) plus a float-rounding pad -- so traversal never prunes a triangle
+// the brute-force closest-hit oracle would pick.  Depth is capped at
+// kMaxDepth so the kernels' fixed LDS traversal stack cannot overflow.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "scene.h"
+
+namespace pt {
+
+namespace {
+
+constexpr int kLeafMax = 4;
+constexpr int kBins = 16;
+constexpr int kMaxDepth = 30;   // kernel stack holds kMaxDepth + 2 entries
+
+struct Box {
+    double lo[3] = {1e300, 1e300, 1e300};
+    double hi[3] = {-1e300, -1e300, -1e300};
+    void grow(const double* p) {
+        for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+    }
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+    }
+    double area() const {
+        double d[3];
+        for (int k = 0; k < 3; k++) d[k] = std::max(0.0, hi[k] - lo[k]);
+        return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+    bool valid() const { return lo[0] <= hi[0]; }
+};
+
+struct Ref { int tri; Box box; double c[3]; };
+
+struct Child { Box box; int link; int count; };   // count 0 = inner node, -1 = empty
+
+struct Builder {
+    Scene& s;
+    std::vector<Ref>& refs;
+    double pad;
+    Builder(Scene& sc, std::vector<Ref>& r, double p) : s(sc), refs(r), pad(p) {}
+
+    static int ceil_log2(long long v) { int d = 0; while ((1LL << d) < v) d++; return d; }
+
+    Child leaf(int b, int e, const Box& box) {
+        Child c;
+        c.box = box;
+        c.link = (int)s.bvh_tri_order.size();
+        c.count = e - b;
+        for (int i = b; i < e; i++) s.bvh_tri_order.push_back(refs[i].tri);
+        return c;
+    }
+
+    Child build(int b, int e, int depth) {
+        Box box, cbox;
+        for (int i = b; i < e; i++) { box.grow(refs[i].box); cbox.grow(refs[i].c); }
+        const int n = e - b;
+        if (n <= kLeafMax) return leaf(b, e, box);
+        // Force balanced splits when the remaining depth budget is tight.
+        const bool force_median = depth + ceil_log2((n + kLeafMax - 1) / kLeafMax) >= kMaxDepth - 1;
+        int axis = 0;
+        double ext = -1;
+        for (int k = 0; k < 3; k++)
+            if (cbox.hi[k] - cbox.lo[k] > ext) { ext = cbox.hi[k] - cbox.lo[k]; axis = k; }
+        int mid = -1;
+        if (!force_median && ext > 0) {
+            double best = 1e300;
+            int best_axis = -1, best_bin = -1;
+            for (int k = 0; k < 3; k++) {
+                double lo = cbox.lo[k], w = cbox.hi[k] - cbox.lo[k];
+                if (!(w > 0)) continue;
+                Box bins[kBins];
+                int cnt[kBins] = {0};
+                for (int i = b; i < e; i++) {
+                    int bi = (int)((refs[i].c[k] - lo) / w * kBins);
+                    bi = std::min(kBins - 1, std::max(0, bi));
+                    cnt[bi]++;
+                    bins[bi].grow(refs[i].box);
+                }
+                double la[kBins], ra[kBins];
+                int lc[kBins], rc[kBins];
+                Box acc; int c = 0;
+                for (int i = 0; i < kBins; i++) { acc.grow(bins[i]); c += cnt[i]; la[i] = acc.valid() ? acc.area() : 0; lc[i] = c; }
+                acc = Box(); c = 0;
+                for (int i = kBins - 1; i >= 0; i--) { acc.grow(bins[i]); c += cnt[i]; ra[i] = acc.valid() ? acc.area() : 0; rc[i] = c; }
+                for (int i = 0; i < kBins - 1; i++) {
+                    if (lc[i] == 0 || rc[i + 1] == 0) continue;
+                    double cost = la[i] * lc[i] + ra[i + 1] * rc[i + 1];
+                    if (cost < best) { best = cost; best_axis = k; best_bin = i; }
+                }
+            }
+            if (best_axis >= 0) {
+                double lo = cbox.lo[best_axis], w = cbox.hi[best_axis] - cbox.lo[best_axis];
+                Ref* p = std::partition(refs.data() + b, refs.data() + e, [&](const Ref& r) {
+                    int bi = (int)((r.c[best_axis] - lo) / w * kBins);
+                    bi = std::min(kBins - 1, std::max(0, bi));
+                    return bi <= best_bin;
+                });
+                mid = (int)(p - refs.data());
+                if (mid == b || mid == e) mid = -1;
+            }
+        }
+        if (mid < 0) {
+            mid = b + n / 2;
+            std::nth_element(refs.begin() + b, refs.begin() + mid, refs.begin() + e,
+                             [&](const Ref& x, const Ref& y) {
+                                 if (x.c[axis] != y.c[axis]) return x.c[axis] < y.c[axis];
+                                 return x.tri < y.tri;
+                             });
+        }
+        int node = (int)s.bvh_nodes.size();
+        s.bvh_nodes.push_back(BvhNode());
+        Child L = build(b, mid, depth + 1);
+        Child R = build(mid, e, depth + 1);
+        store(node, L, R);
+        Child c;
+        c.box = box;
+        c.link = node;
+        c.count = 0;
+        return c;
+    }
+
+    void put(const Box& bx, float* lo, float* hi) {
+        for (int k = 0; k < 3; k++) {
+            // round outward to float and pad
+            float l = (float)(bx.lo[k] - pad), h = (float)(bx.hi[k] + pad);
+            if ((double)l > bx.lo[k] - pad) l = std::nextafter(l, -INFINITY);
+            if ((double)h < bx.hi[k] + pad) h = std::nextafter(h, INFINITY);
+            lo[k] = l; hi[k] = h;
+        }
+    }
+
+    void store(int node, const Child& L, const Child& R) {
+        BvhNode& nd = s.bvh_nodes[node];
+        std::memset(&nd, 0, sizeof nd);
+        if (L.count >= 0) put(L.box, nd.lo0, nd.hi0);
+        if (R.count >= 0) put(R.box, nd.lo1, nd.hi1);
+        nd.link0 = L.link; nd.count0 = L.count;
+        nd.link1 = R.link; nd.count1 = R.count;
+        if (L.count < 0) { for (int k = 0; k < 3; k++) { nd.lo0[k] = 1.0f; nd.hi0[k] = -1.0f; } }
+        if (R.count < 0) { for (int k = 0; k < 3; k++) { nd.lo1[k] = 1.0f; nd.hi1[k] = -1.0f; } }
+    }
+};
+
+}  // namespace
+
+void Scene::buildBvh(int mesh) {
+    const Mesh& m = meshes[mesh];
+    const int ts = m.triangle_indices.start_index, te = m.triangle_indices.end_index;
+    std::vector<Ref> refs;
+    refs.reserve(te - ts);
+    const double e = (double)kEps;
+    double diag = 0;
+    {
+        const BoundingBox& bb = m.bounding_box;
+        if (te > ts) {
+            double dx = (double)bb.max.x - bb.min.x, dy = (double)bb.max.y - bb.min.y, dz = (double)bb.max.z - bb.min.z;
+            diag = std::sqrt(dx * dx + dy * dy + dz * dz);
+        }
+    }
+    for (int t = ts; t < te; t++) {
+        const f3 a = vertices[triangles[t].vertex_indices[0]].position;
+        const f3 b = vertices[triangles[t].vertex_indices[1]].position;
+        const f3 c = vertices[triangles[t].vertex_indices[2]].position;
+        const double v0[3] = {a.x, a.y, a.z};
+        const double e1[3] = {(double)b.x - a.x, (double)b.y - a.y, (double)b.z - a.z};
+        const double e2[3] = {(double)c.x - a.x, (double)c.y - a.y, (double)c.z - a.z};
+        // accepted region: u >= -e, v >= -e, u + v <= 1 + e  -> corners
+        const double uv[3][2] = {{-e, -e}, {1 + 2 * e, -e}, {-e, 1 + 2 * e}};
+        Ref r;
+        r.tri = t;
+        double cen[3] = {0, 0, 0};
+        for (int q = 0; q < 3; q++) {
+            double p[3];
+            for (int k = 0; k < 3; k++) p[k] = v0[k] + uv[q][0] * e1[k] + uv[q][1] * e2[k];
+            r.box.grow(p);
+        }
+        const double tri_v[3][3] = {{a.x, a.y, a.z}, {b.x, b.y, b.z}, {c.x, c.y, c.z}};
+        for (int q = 0; q < 3; q++)
+            for (int k = 0; k < 3; k++) cen[k] += tri_v[q][k] / 3.0;
+        for (int k = 0; k < 3; k++) r.c[k] = cen[k];
+        // non-finite geometry: make the box cover everything
+        bool finite = true;
+        for (int k = 0; k < 3; k++) finite &= std::isfinite(r.box.lo[k]) && std::isfinite(r.box.hi[k]);
+        if (!finite) {
+            for (int k = 0; k < 3; k++) { r.box.lo[k] = -3e38; r.box.hi[k] = 3e38; r.c[k] = 0; }
+        }
+        refs.push_back(r);
+    }
+    // Rounding pad: 1e-4 of the mesh diagonal (the triangle test's float error
+    // is ~1e-7 relative to the ray-to-triangle distance) plus an absolute floor.
+    const double pad = 1e-4 * diag + 1e-3;
+    Builder B(*this, refs, pad);
+    int root;
+    if (refs.empty()) {
+        root = (int)bvh_nodes.size();
+        bvh_nodes.push_back(BvhNode());
+        Child E; E.link = -1; E.count = -1;
+        B.store(root, E, E);
+    } else {
+        Child c = B.build(0, (int)refs.size(), 1);
+        if (c.count > 0) {
+            root = (int)bvh_nodes.size();
+            bvh_nodes.push_back(BvhNode());
+            Child E; E.link = -1; E.count = -1;
+            B.store(root, c, E);
+        } else {
+            root = c.link;
+        }
+    }
+    mesh_bvh_root[mesh] = root;
+}
+
+}  // namespace pt

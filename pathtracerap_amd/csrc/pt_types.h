@@ -1,0 +1,50 @@
+// pt_types.h -- POD records shared by the host scene builder and the kernels.
+#pragma once
+
+#include "pt_math.h"
+
+namespace pt {
+
+// Primitive.h:252-257 SpatialAcceleration::EntityType
+enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2, ENTITY_SPHERE = 3 };
+
+// Acceleration structure used by the intersect stage.
+//  ACCEL_GRID: the reference's per-mesh uniform grid + 3D-DDA with its
+//              "2 voxels past the last hit" early exit (Renderer.cpp:238-360);
+//              bit-exact with the reference algorithm.
+//  ACCEL_BVH : MI355X BLAS per mesh (binned SAH, 2-wide nodes, LDS stacks),
+//              exact closest hit with the reference's triangle test; equals
+//              the grid result except where the grid's early exit misses a
+//              nearer triangle.
+enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1 };
+
+// One instance (Model, Primitive.h:237-244) flattened for the kernels.
+// 52 dwords; read with wave-uniform (scalar) loads inside the model loop.
+struct ModelRec {
+    float w2m[12];        // world_to_model columns 0..3, rows 0..2 (m[c*3+k])
+    float m2w[12];        // model_to_world, same packing
+    float nm[9];          // inverse(mat3(model_to_world)): nm[r*3+c] = Inverse[r][c]
+    int mat_type;         // Material::MaterialType
+    float bbox[6];        // mesh bounding box (model space) min3 max3
+    float vw[3];          // grid voxel widths
+    int vox_start;        // grid->voxelIndices.start_index
+    int mesh;
+    int tri_start, tri_end;
+    int bvh_root;         // index of the mesh's BLAS root node
+    float color[3];       // Material::color
+    int pad_;
+};
+static_assert(sizeof(ModelRec) == 52 * 4, "ModelRec layout");
+
+// 2-wide BVH node: both children's boxes in one 64-byte line.
+// link/count: count == 0 -> link is a child node index; count > 0 -> link is
+// the first entry of bvh_tri_order and count the number of triangles.
+struct BvhNode {
+    float lo0[3]; int link0;
+    float hi0[3]; int link1;
+    float lo1[3]; int count0;
+    float hi1[3]; int count1;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
+
+}  // namespace pt

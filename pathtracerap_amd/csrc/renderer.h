@@ -1,0 +1,106 @@
+// renderer.h -- MI355X wavefront renderer (Renderer.h:368-377 mirror).
+//
+// allocateOnGPU / renderLoop / renderImage / free keep the reference's
+// entry points; underneath, each bounce is ONE fused gfx950 kernel
+// (intersect + BSDF scatter + block-local stable compaction + framebuffer
+// accumulate of terminated rays) followed by a one-workgroup block-offset
+// scan -- no host round trip inside an iteration.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "scene.h"
+
+namespace pt {
+
+struct RenderConfig {            // Config.h + generateRaysKernel constants, at runtime
+    int width = 1000, height = 800;       // RESOLUTION_X/Y
+    int iterations = 500;                 // ITER
+    int max_bounces = 5;                  // Renderer.cpp:550
+    int accel = ACCEL_GRID;
+    int grid[3] = {25, 25, 25};           // GRID_X/Y/Z
+    int tail_drop = 0;                    // replicate ceil(n/32) launch truncation (Renderer.cpp:573)
+    double cam[3] = {0.0, 0.0, 920.0};    // Renderer.cpp:528
+    double plane_z = 900.0;               // Renderer.cpp:543
+    double plane_x0 = -10.0, plane_y0 = -4.0, plane_w = 20.0, plane_h = 16.0;  // Renderer.cpp:538-542
+};
+
+// Everything a kernel needs, passed by value as the kernel argument.
+struct KParams {
+    // scene (read-only, stays L2/MALL resident)
+    const ModelRec* models;
+    int nmodels;
+    int gdim[3];
+    const float4* tri_geom;     // 3 float4 per triangle: v0, e1, e2
+    const float4* tri_normal;   // 1 float4 per triangle
+    const int2* voxels;         // (start, end)
+    const int* per_voxel;
+    const BvhNode* bvh;
+    const int* bvh_tri;
+    // frame
+    int width, height, npix, max_bounces, nblocks;
+    float step_x, step_y, cam_x, cam_y, cam_z, plane_z;
+    double plane_x0, plane_y0;
+    float4* ray[2][3];          // ping-pong SoA planes: (o, pixel) (d, bounces) (color, -)
+    float4* cache_hit;          // primary hit: dist, normal
+    int* cache_model;
+    float* image;               // W*H*3 accumulator (Pixel::color)
+    int* blk_cnt;
+    int* blk_off;
+    int* dst_start;
+    int* n_live;                // live rays per bounce
+    unsigned long long* segments;
+};
+
+struct KernelStats {
+    double bounce_ms = 0, scan_ms = 0, primary_ms = 0;
+    long long bounce_launches = 0, scan_launches = 0;
+};
+
+class Renderer {
+public:
+    explicit Renderer(const RenderConfig& cfg);
+    ~Renderer();
+    int allocateOnGPU(const Scene& scene);          // Renderer.cpp:65-130
+    int clearImage();                                // initImageKernel (Renderer.cpp:557-565)
+    int renderLoop(int first_iter, int n_iters);     // Renderer.cpp:567-648 (asynchronous)
+    int renderImage(const std::string& path, int iterations_total);  // Renderer.cpp:15-63
+    int readImage(float* host_rgb);
+    int synchronize();
+    void free();                                     // Renderer.cpp:132-148
+
+    int setStream(hipStream_t s);
+    int bindImage(float* device_rgb);
+    int setProfiling(bool on);
+    int kernelStats(KernelStats* out);
+    long long segments();
+    int primaryHits(float* dist, float* normal, int* model);
+    int intersectRays(int n, const float* orig, const float* dir, float* dist, float* normal, int* model);
+
+    RenderConfig cfg;
+    std::string last_error;
+
+private:
+    int launchPrimary();
+    int fail(hipError_t e, const char* what);
+    void freeBuffers();
+
+    KParams kp{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool allocated = false;
+    bool cache_valid = false;        // is_first_intersection_cached (Renderer.cpp:580)
+    bool external_image = false;
+    bool profiling = false;
+    std::vector<void*> allocs;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, scan_events;
+    KernelStats stats;
+};
+
+// Device math conformance hook (pt_selftest_math).
+int selftest_math(int n, const float* x, const float* y, float* out, std::string* err);
+
+}  // namespace pt

@@ -1,0 +1,756 @@
+// renderer.hip -- gfx950 kernels + Renderer host code.
+//
+// Per iteration (one sample per pixel, Renderer.cpp:582-644):
+//   bounce 0 : k_bounce<first>  -- camera ray + cached primary hit -> shade ->
+//              compact survivors (block-local, stable) / accumulate the dead
+//   scan     : k_scan           -- one workgroup: exclusive scan of the block
+//              survivor counts -> dense slot numbering for the next bounce
+//   bounce b : k_bounce<rest>   -- gather ray (slot j -> source via the scan),
+//              intersect (grid DDA or BVH), shade, compact / accumulate
+// The dense slot j of a ray at bounce b equals its index in the reference's
+// thrust::stable_partition'ed ray pool, so the RNG seed
+// makeSeededRandomEngine(iter, j, remaining_bounces) -- and hence every
+// sample -- is identical to the reference algorithm's.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+
+#include "renderer.h"
+
+#pragma clang fp contract(off)
+
+namespace pt {
+
+constexpr int kBlock = 256;
+constexpr int kStack = 32;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+struct Hit { float dist; f3 n; int model; };
+
+// computeRayBoundingBoxIntersection (Renderer.cpp:150-170)
+__device__ __forceinline__ bool slab_ref(const float* bb, f3 o, f3 d, f3 inv, float& t) {
+    float t1 = d.x == 0.0f ? kFMin : (bb[0] - o.x) * inv.x;
+    float t2 = d.x == 0.0f ? kFMax : (bb[3] - o.x) * inv.x;
+    float t3 = d.y == 0.0f ? kFMin : (bb[1] - o.y) * inv.y;
+    float t4 = d.y == 0.0f ? kFMax : (bb[4] - o.y) * inv.y;
+    float t5 = d.z == 0.0f ? kFMin : (bb[2] - o.z) * inv.z;
+    float t6 = d.z == 0.0f ? kFMax : (bb[5] - o.z) * inv.z;
+    float tmin = fmaxf(fmaxf(fminf(t1, t2), fminf(t3, t4)), fminf(t5, t6));
+    float tmax = fminf(fminf(fmaxf(t1, t2), fmaxf(t3, t4)), fmaxf(t5, t6));
+    if (tmax < 0 || tmin > tmax) return false;
+    t = tmin;
+    return true;
+}
+
+// computeRayTriangleIntersection (Renderer.cpp:174-215), edges precomputed.
+// Returns true when the test passes; *t_out is the hit distance.
+__device__ __forceinline__ bool tri_test(const float4* __restrict__ tg, int it, f3 o, f3 d, float& t_out) {
+    const float4 A = tg[3 * it + 0];
+    const float4 B = tg[3 * it + 1];
+    const float4 C = tg[3 * it + 2];
+    const f3 v0 = mk3(A.x, A.y, A.z), e1 = mk3(B.x, B.y, B.z), e2 = mk3(C.x, C.y, C.z);
+    f3 pvec = cross(d, e2);
+    float det = dot(e1, pvec);
+    if (absr(det - 0.0f) < kEps) return false;
+    float inv_det = 1 / det;
+    f3 tvec = o - v0;
+    float u = dot(tvec, pvec) * inv_det;
+    if (u < 0.0f - kEps || u > 1.0f + kEps) return false;
+    f3 qvec = cross(tvec, e1);
+    float v = dot(d, qvec) * inv_det;
+    if (v < 0.0f - kEps || u + v > 1.0f + kEps) return false;
+    float t = dot(e2, qvec) * inv_det;
+    if (t < 0.0f - kEps) return false;
+    t_out = t;
+    return true;
+}
+
+// computeRayGridIntersection (Renderer.cpp:238-360): 3D-DDA over the model's
+// uniform grid, stop 3 voxels past the last voxel that produced a hit.
+__device__ bool grid_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, float& best, int& best_tri) {
+    const int GX = p.gdim[0], GY = p.gdim[1], GZ = p.gdim[2];
+    float t_box;
+    if (!slab_ref(M.bbox, o, d, inv, t_box)) return false;
+    f3 pt = o + d * t_box;
+    if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) return false;
+    int ix = f2i_sat(absr(pt.x - M.bbox[0] + kEps) / M.vw[0]);
+    int iy = f2i_sat(absr(pt.y - M.bbox[1] + kEps) / M.vw[1]);
+    int iz = f2i_sat(absr(pt.z - M.bbox[2] + kEps) / M.vw[2]);
+    ix = ix < 0 ? 0 : (ix > GX - 1 ? GX - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > GY - 1 ? GY - 1 : iy);
+    iz = iz < 0 ? 0 : (iz > GZ - 1 ? GZ - 1 : iz);
+    f3 tmax = mk3(kFMax, kFMax, kFMax), delta = mk3(kFMax, kFMax, kFMax);
+    const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
+    const int ox = d.x > 0.0f ? GX : -1, oy = d.y > 0.0f ? GY : -1, oz = d.z > 0.0f ? GZ : -1;
+    const int nx = d.x > 0.0f ? ix + 1 : ix, ny = d.y > 0.0f ? iy + 1 : iy, nz = d.z > 0.0f ? iz + 1 : iz;
+    const float px = M.bbox[0] + (float)nx * M.vw[0];
+    const float py = M.bbox[1] + (float)ny * M.vw[1];
+    const float pz = M.bbox[2] + (float)nz * M.vw[2];
+    if (d.x != 0) { delta.x = absr(M.vw[0] * inv.x); tmax.x = (px - pt.x) * inv.x; }
+    if (d.y != 0) { delta.y = absr(M.vw[1] * inv.y); tmax.y = (py - pt.y) * inv.y; }
+    if (d.z != 0) { delta.z = absr(M.vw[2] * inv.z); tmax.z = (pz - pt.z) * inv.z; }
+    int cx = 0, cy = 0, cz = 0;
+    bool hit = false;
+    const int plane = GX * GY;
+    for (;;) {
+        const int2 vr = p.voxels[M.vox_start + ix + iy * GX + iz * plane];
+        bool vhit = false;
+        for (int i = vr.x; i < vr.y; i++) {
+            const int it = p.per_voxel[i];
+            float t;
+            if (tri_test(p.tri_geom, it, o, d, t)) {
+                vhit = true;
+                if (best > t) { best = t; best_tri = it; }
+            }
+        }
+        if (vhit) { cx = ix; cy = iy; cz = iz; hit = true; }
+        if (hit && (iabs(cx - ix) > 2 || iabs(cy - iy) > 2 || iabs(cz - iz) > 2)) return true;
+        if (tmax.x < tmax.y && tmax.x < tmax.z) {
+            ix += sx;
+            if (ix == ox || tmax.x >= kFMax) return hit;
+            tmax.x += delta.x;
+        } else if (tmax.y < tmax.z) {
+            iy += sy;
+            if (iy == oy || tmax.y >= kFMax) return hit;
+            tmax.y += delta.y;
+        } else {
+            iz += sz;
+            if (iz == oz || tmax.z >= kFMax) return hit;
+            tmax.z += delta.z;
+        }
+    }
+}
+
+// Conservative slab test for BVH node boxes (boxes are padded at build time).
+__device__ __forceinline__ void node_slab(const float* lo, const float* hi, f3 o, f3 inv, float& tn, float& tf) {
+    float a0 = (lo[0] - o.x) * inv.x, b0 = (hi[0] - o.x) * inv.x;
+    float a1 = (lo[1] - o.y) * inv.y, b1 = (hi[1] - o.y) * inv.y;
+    float a2 = (lo[2] - o.z) * inv.z, b2 = (hi[2] - o.z) * inv.z;
+    tn = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fminf(a2, b2));
+    tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
+}
+
+// Exact closest hit over the mesh's triangles via its BLAS.  Matches the
+// brute-force scan in triangle-index order: (t, index) lexicographic minimum.
+__device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, float& best, int& best_tri,
+                            int* __restrict__ stack) {
+    bool any = false;
+    int sp = 0;
+    int cur = M.bvh_root;
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+    for (;;) {
+        const float4 q0 = nodes[4 * cur + 0];
+        const float4 q1 = nodes[4 * cur + 1];
+        const float4 q2 = nodes[4 * cur + 2];
+        const float4 q3 = nodes[4 * cur + 3];
+        const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+        const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+        const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+        const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+        float tn0, tf0, tn1, tf1;
+        node_slab(lo0, hi0, o, inv, tn0, tf0);
+        node_slab(lo1, hi1, o, inv, tn1, tf1);
+        bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
+        bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
+        if (h0 && cnt0 > 0) {
+            for (int i = link0; i < link0 + cnt0; i++) {
+                const int it = p.bvh_tri[i];
+                float t;
+                if (tri_test(p.tri_geom, it, o, d, t)) {
+                    any = true;
+                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+                }
+            }
+            h0 = false;
+        }
+        if (h1 && cnt1 > 0) {
+            for (int i = link1; i < link1 + cnt1; i++) {
+                const int it = p.bvh_tri[i];
+                float t;
+                if (tri_test(p.tri_geom, it, o, d, t)) {
+                    any = true;
+                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+                }
+            }
+            h1 = false;
+        }
+        if (h0 && h1) {
+            const bool first0 = tn0 <= tn1;
+            stack[sp * kBlock] = first0 ? link1 : link0;
+            sp++;
+            cur = first0 ? link0 : link1;
+        } else if (h0) {
+            cur = link0;
+        } else if (h1) {
+            cur = link1;
+        } else {
+            if (sp == 0) break;
+            sp--;
+            cur = stack[sp * kBlock];
+        }
+    }
+    return any;
+}
+
+// computeRaySceneIntersectionKernel body (Renderer.cpp:364-409) for one ray.
+template <int ACCEL>
+__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack) {
+    float gdist = kFMax;
+    int gmodel = -1, gtri = -1;
+    for (int im = 0; im < p.nmodels; im++) {
+        const ModelRec& M = p.models[im];
+        const f3 o = xform12(M.w2m, orig, 1.0f);
+        const f3 d = normalize(xform12(M.w2m, dir, 0.0f));
+        const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+        float best = kFMax;
+        int best_tri = -1;
+        bool ok;
+        if (ACCEL == ACCEL_GRID) ok = grid_closest(p, M, o, d, inv, best, best_tri);
+        else ok = bvh_closest(p, M, o, d, inv, best, best_tri, stack);
+        if (ok) {
+            const f3 nd = normalize(d);
+            const f3 pm = o + nd * best;
+            const f3 pw = xform12(M.m2w, pm, 1.0f);
+            const float dd = length(pw - orig);
+            if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
+        }
+    }
+    Hit h;
+    h.dist = kFMax;
+    h.n = mk3(0, 0, 0);
+    h.model = -1;
+    if (gdist < kFMax) {
+        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
+        h.dist = gdist;
+        h.model = gmodel;
+        h.n = normalize(xform_normal9(p.models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
+    }
+    return h;
+}
+
+// generateRaysKernel (Renderer.cpp:521-555)
+__device__ __forceinline__ void camera_ray(const KParams& p, int i, f3& o, f3& d) {
+    const int y = i / p.width, x = i % p.width;
+    const float wx = (float)(p.plane_x0 + (double)((float)x * p.step_x));
+    const float wy = (float)(p.plane_y0 + (double)((float)y * p.step_y));
+    o = mk3(p.cam_x, p.cam_y, p.cam_z);
+    d = mk3(wx, wy, p.plane_z) - o;
+}
+
+struct RayState { f3 o, d, c; int pixel, bounces; };
+
+// shadeRayKernel (Renderer.cpp:411-479) for one ray; slot = iray.
+__device__ __forceinline__ void shade(const KParams& p, RayState& r, const Hit& h, int iter, int slot) {
+    if (r.bounces <= 0) r.c = r.c * mk3(0.01f, 0.01f, 0.01f);
+    if (h.dist < kFMax) {
+        const f3 dir = normalize(r.d);
+        const f3 ip = r.o + dir * h.dist;
+        if (r.bounces > 0) {
+            const ModelRec& M = p.models[h.model];
+            const int mt = M.mat_type;
+            const f3 mc = mk3(M.color[0], M.color[1], M.color[2]);
+            if (mt == MAT_DIFFUSE || mt == MAT_METAL || mt == MAT_COAT) {
+                Rng rng = Rng::make(iter, slot, r.bounces);
+                if (mt == MAT_DIFFUSE) r.d = scatter_hemisphere(h.n, rng);
+                else if (mt == MAT_METAL) r.d = scatter_metal(h.n, dir, rng);
+                else r.d = scatter_coat(h.n, dir, rng);
+                r.o = ip + h.n * 0.1f;
+                r.c = r.c * mc;
+            } else if (mt == MAT_EMISSIVE) {
+                r.bounces = 0;
+                r.c = r.c * mc;
+                return;
+            } else if (mt == MAT_REFLECTIVE) {
+                r.c = r.c * mc;
+                const f3 rr = reflect_ref(dir, h.n);
+                r.o = ip + h.n * 0.1f;
+                r.d = rr;
+            }
+        }
+    } else {
+        r.bounces = 0;
+        r.c = r.c * mk3(0.01f, 0.01f, 0.01f);
+        return;
+    }
+    r.bounces--;
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+
+// Primary intersections, cached once per renderer (Renderer.cpp:596-613).
+template <int ACCEL>
+__global__ __launch_bounds__(kBlock) void k_primary(KParams p) {
+    __shared__ int s_stack[ACCEL == ACCEL_BVH ? kStack * kBlock : 1];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.npix) return;
+    f3 o, d;
+    camera_ray(p, i, o, d);
+    const Hit h = intersect_scene<ACCEL>(p, o, d, s_stack + threadIdx.x);
+    p.cache_hit[i] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+    p.cache_model[i] = h.model;
+}
+
+// Test hook: intersect an arbitrary batch of world-space rays.
+template <int ACCEL>
+__global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, const float* orig, const float* dir,
+                                                           float* dist, float* nrm, int* model) {
+    __shared__ int s_stack[ACCEL == ACCEL_BVH ? kStack * kBlock : 1];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const Hit h = intersect_scene<ACCEL>(p, mk3(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]),
+                                         mk3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), s_stack + threadIdx.x);
+    dist[i] = h.dist;
+    nrm[3 * i] = h.n.x; nrm[3 * i + 1] = h.n.y; nrm[3 * i + 2] = h.n.z;
+    model[i] = h.model;
+}
+
+// One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
+template <bool FIRST, int ACCEL>
+__global__ __launch_bounds__(kBlock) void k_bounce(KParams p, int iter, int bounce) {
+    __shared__ int s_stack[(!FIRST && ACCEL == ACCEL_BVH) ? kStack * kBlock : 1];
+    __shared__ int s_wave[kBlock / 64];
+    const int n = FIRST ? p.npix : p.n_live[bounce];
+    const int j0 = blockIdx.x * kBlock;
+    if (j0 >= n) return;                       // whole block idle (uniform)
+    const int j = j0 + threadIdx.x;
+    const bool active = j < n;
+    const int in_buf = (bounce + 1) & 1, out_buf = bounce & 1;
+
+    RayState r;
+    Hit h;
+    if (active) {
+        if (FIRST) {
+            camera_ray(p, j, r.o, r.d);
+            r.c = mk3(1.0f, 1.0f, 1.0f);
+            r.pixel = j;
+            r.bounces = p.max_bounces;
+            const float4 ch = p.cache_hit[j];
+            h.dist = ch.x;
+            h.n = mk3(ch.y, ch.z, ch.w);
+            h.model = p.cache_model[j];
+        } else {
+            // dense slot j -> (source block b, rank) via the scan of the previous bounce
+            int lo = p.dst_start[blockIdx.x], hi = p.dst_start[blockIdx.x + 1];
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
+            }
+            const int src = lo * kBlock + (j - p.blk_off[lo]);
+            const float4 a = p.ray[in_buf][0][src];
+            const float4 b = p.ray[in_buf][1][src];
+            const float4 c = p.ray[in_buf][2][src];
+            r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
+            r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
+            r.c = mk3(c.x, c.y, c.z);
+            h = intersect_scene<ACCEL>(p, r.o, r.d, s_stack + threadIdx.x);
+        }
+        shade(p, r, h, iter, j);
+    }
+    const bool alive = active && r.bounces > 0;
+    if (active && !alive) {
+        // gatherImageDataKernel (Renderer.cpp:481-496): pixel += 1.0f * sqrt(color).
+        // Each pixel has exactly one ray per iteration: no atomics needed.
+        float* px = p.image + 3 * (size_t)r.pixel;
+        px[0] += 1.0f * sqrtf(r.c.x);
+        px[1] += 1.0f * sqrtf(r.c.y);
+        px[2] += 1.0f * sqrtf(r.c.z);
+    }
+    // Block-local stable compaction (ballot + wave prefix), order == slot order.
+    const unsigned long long m = __ballot(alive);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[wid] = __popcll(m);
+    __syncthreads();
+    int base = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; w++) {
+        const int c = s_wave[w];
+        base += (w < wid) ? c : 0;
+        total += c;
+    }
+    if (alive) {
+        const int dst = j0 + base + rank;
+        p.ray[out_buf][0][dst] = make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(r.pixel));
+        p.ray[out_buf][1][dst] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(r.bounces));
+        p.ray[out_buf][2][dst] = make_float4(r.c.x, r.c.y, r.c.z, 0.0f);
+    }
+    if (threadIdx.x == 0) p.blk_cnt[blockIdx.x] = total;
+}
+
+// One workgroup: exclusive scan of survivor counts of bounce `bounce`,
+// live count for bounce+1, and the first source block of every
+// destination block (dst_start).
+__global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
+    __shared__ int s_part[1024];
+    __shared__ int s_total;
+    const int tid = threadIdx.x;
+    const int n = bounce == 0 ? p.npix : p.n_live[bounce];
+    const int nb = (n + kBlock - 1) / kBlock;
+    const int per = (nb + 1023) / 1024;
+    const int s = tid * per, e = min(s + per, nb);
+    int sum = 0;
+    for (int i = s; i < e; i++) sum += p.blk_cnt[i];
+    s_part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int v = tid >= off ? s_part[tid - off] : 0;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
+    }
+    int acc = s_part[tid] - sum;   // exclusive
+    for (int i = s; i < e; i++) { p.blk_off[i] = acc; acc += p.blk_cnt[i]; }
+    if (tid == 1023) {
+        s_total = s_part[1023];
+        p.blk_off[nb] = s_part[1023];
+        p.n_live[bounce + 1] = s_part[1023];
+        p.segments[0] += (unsigned long long)n;
+    }
+    __syncthreads();
+    const int total = s_total;
+    for (int i = s; i < e; i++) {
+        const int c = p.blk_cnt[i];
+        if (c == 0) continue;
+        const int o0 = p.blk_off[i];
+        for (int bd = (o0 + kBlock - 1) / kBlock; bd * kBlock < o0 + c; bd++) p.dst_start[bd] = i;
+    }
+    if (tid == 0) p.dst_start[(total + kBlock - 1) / kBlock] = nb > 0 ? nb - 1 : 0;
+}
+
+__global__ void k_selftest_math(int n, const float* x, const float* y, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float sv, cv;
+    sincos_ref(x[i], &sv, &cv);
+    out[5 * i + 0] = sv;
+    out[5 * i + 1] = cv;
+    out[5 * i + 2] = powf_ref(x[i], y[i]);
+    out[5 * i + 3] = sqrtf(x[i]);
+    out[5 * i + 4] = x[i] / y[i];
+}
+
+__global__ void k_zero(float* a, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = 0.0f;
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+Renderer::Renderer(const RenderConfig& c) : cfg(c) {}
+Renderer::~Renderer() { free(); }
+
+int Renderer::fail(hipError_t e, const char* what) {
+    last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return -1;
+}
+
+#define PT_HIP(call)                                   \
+    do {                                               \
+        hipError_t _e = (call);                        \
+        if (_e != hipSuccess) return fail(_e, #call);  \
+    } while (0)
+
+int Renderer::setStream(hipStream_t s) {
+    if (own_stream && stream) hipStreamDestroy(stream);
+    stream = s;
+    own_stream = false;
+    return 0;
+}
+
+int Renderer::bindImage(float* device_rgb) {
+    kp.image = device_rgb;
+    external_image = device_rgb != nullptr;
+    return 0;
+}
+
+template <typename T>
+static hipError_t upload(std::vector<void*>& allocs, T** dst, const void* src, size_t bytes, hipStream_t s) {
+    void* d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes ? bytes : 16);
+    if (e != hipSuccess) return e;
+    allocs.push_back(d);
+    if (bytes && src) e = hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, s);
+    *dst = (T*)d;
+    return e;
+}
+
+int Renderer::allocateOnGPU(const Scene& scene) {
+    if (!scene.built) { last_error = "scene not built (call build first)"; return -1; }
+    if (cfg.width <= 0 || cfg.height <= 0) { last_error = "bad resolution"; return -1; }
+    if ((long long)cfg.width * cfg.height > (1LL << 30)) { last_error = "resolution too large"; return -1; }
+    for (int k = 0; k < 3; k++)
+        if (cfg.grid[k] != scene.grid_dim[k]) { last_error = "config grid dims differ from the scene build"; return -1; }
+    if (cfg.accel == ACCEL_BVH && scene.bvh_nodes.empty()) { last_error = "scene built without BVH"; return -1; }
+    for (const Voxel& v : scene.voxels)
+        if (v.entity_type != ENTITY_TRIANGLE) { last_error = "unsupported voxel entity type"; return -1; }
+    freeBuffers();
+    if (!stream) {
+        PT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        own_stream = true;
+    }
+    kp = KParams{};
+    kp.nmodels = (int)scene.model_recs.size();
+    for (int k = 0; k < 3; k++) kp.gdim[k] = scene.grid_dim[k];
+    PT_HIP(upload(allocs, &kp.models, scene.model_recs.data(), scene.model_recs.size() * sizeof(ModelRec), stream));
+    PT_HIP(upload(allocs, &kp.tri_geom, scene.tri_geom.data(), scene.tri_geom.size() * sizeof(float), stream));
+    PT_HIP(upload(allocs, &kp.tri_normal, scene.tri_normal.data(), scene.tri_normal.size() * sizeof(float), stream));
+    std::vector<int2> vox(scene.voxels.size());
+    for (size_t i = 0; i < vox.size(); i++)
+        vox[i] = make_int2(scene.voxels[i].entity_index_range.start_index, scene.voxels[i].entity_index_range.end_index);
+    PT_HIP(upload(allocs, &kp.voxels, vox.data(), vox.size() * sizeof(int2), stream));
+    PT_HIP(upload(allocs, &kp.per_voxel, scene.per_voxel_data_pool.data(), scene.per_voxel_data_pool.size() * sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
+    PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
+
+    kp.width = cfg.width;
+    kp.height = cfg.height;
+    const int npix_all = cfg.width * cfg.height;
+    kp.npix = cfg.tail_drop ? (npix_all / 32) * 32 : npix_all;
+    kp.max_bounces = cfg.max_bounces;
+    kp.nblocks = (npix_all + kBlock - 1) / kBlock;
+    kp.step_x = (float)(cfg.plane_w / cfg.width);
+    kp.step_y = (float)(cfg.plane_h / cfg.height);
+    kp.cam_x = (float)cfg.cam[0]; kp.cam_y = (float)cfg.cam[1]; kp.cam_z = (float)cfg.cam[2];
+    kp.plane_z = (float)cfg.plane_z;
+    kp.plane_x0 = cfg.plane_x0;
+    kp.plane_y0 = cfg.plane_y0;
+    const size_t cap = (size_t)kp.nblocks * kBlock;
+    for (int b = 0; b < 2; b++)
+        for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &kp.ray[b][q], nullptr, cap * sizeof(float4), stream));
+    PT_HIP(upload(allocs, &kp.cache_hit, nullptr, cap * sizeof(float4), stream));
+    PT_HIP(upload(allocs, &kp.cache_model, nullptr, cap * sizeof(int), stream));
+    if (!external_image) PT_HIP(upload(allocs, &kp.image, nullptr, (size_t)npix_all * 3 * sizeof(float), stream));
+    PT_HIP(upload(allocs, &kp.blk_cnt, nullptr, (kp.nblocks + 1) * sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.blk_off, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.dst_start, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.n_live, nullptr, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
+    PT_HIP(hipStreamSynchronize(stream));
+    allocated = true;
+    cache_valid = false;
+    return clearImage();
+}
+
+int Renderer::clearImage() {
+    if (!allocated) { last_error = "not allocated"; return -1; }
+    const size_t n = (size_t)cfg.width * cfg.height * 3;
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, kp.image, n);
+    PT_HIP(hipGetLastError());
+    return 0;
+}
+
+int Renderer::launchPrimary() {
+    const dim3 grid((unsigned)((kp.npix + kBlock - 1) / kBlock));
+    if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL(k_primary<ACCEL_BVH>, grid, dim3(kBlock), 0, stream, kp);
+    else hipLaunchKernelGGL(k_primary<ACCEL_GRID>, grid, dim3(kBlock), 0, stream, kp);
+    PT_HIP(hipGetLastError());
+    cache_valid = true;
+    return 0;
+}
+
+int Renderer::renderLoop(int first_iter, int n_iters) {
+    if (!allocated) { last_error = "renderLoop before allocateOnGPU"; return -1; }
+    if (n_iters < 0 || first_iter < 0) { last_error = "bad iteration range"; return -1; }
+    if (kp.npix == 0) return 0;
+    if (!cache_valid) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
+        if (launchPrimary() != 0) return -1;
+        if (profiling) {
+            hipEventRecord(e1, stream);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            stats.primary_ms += ms;
+            hipEventDestroy(e0); hipEventDestroy(e1);
+        }
+    }
+    const dim3 grid((unsigned)kp.nblocks), block(kBlock);
+    const int passes = cfg.max_bounces > 1 ? cfg.max_bounces : 1;
+    for (int it = 0; it < n_iters; it++) {
+        const int iter = first_iter + it;
+        for (int b = 0; b < passes; b++) {
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
+            if (b == 0) {
+                if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<true, ACCEL_BVH>), grid, block, 0, stream, kp, iter, b);
+                else hipLaunchKernelGGL((k_bounce<true, ACCEL_GRID>), grid, block, 0, stream, kp, iter, b);
+            } else {
+                if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<false, ACCEL_BVH>), grid, block, 0, stream, kp, iter, b);
+                else hipLaunchKernelGGL((k_bounce<false, ACCEL_GRID>), grid, block, 0, stream, kp, iter, b);
+            }
+            PT_HIP(hipGetLastError());
+            if (profiling) { hipEventRecord(e1, stream); bounce_events.push_back({e0, e1}); e0 = e1 = nullptr; }
+            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, stream, kp, b);
+            PT_HIP(hipGetLastError());
+            if (profiling) { hipEventRecord(e1, stream); scan_events.push_back({e0, e1}); }
+        }
+    }
+    return 0;
+}
+
+int Renderer::synchronize() {
+    if (!stream) return 0;
+    PT_HIP(hipStreamSynchronize(stream));
+    return 0;
+}
+
+int Renderer::setProfiling(bool on) {
+    profiling = on;
+    return 0;
+}
+
+int Renderer::kernelStats(KernelStats* out) {
+    PT_HIP(hipStreamSynchronize(stream));
+    for (auto& ev : bounce_events) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev.first, ev.second);
+        stats.bounce_ms += ms;
+        stats.bounce_launches++;
+        hipEventDestroy(ev.first); hipEventDestroy(ev.second);
+    }
+    for (auto& ev : scan_events) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev.first, ev.second);
+        stats.scan_ms += ms;
+        stats.scan_launches++;
+        hipEventDestroy(ev.first); hipEventDestroy(ev.second);
+    }
+    bounce_events.clear();
+    scan_events.clear();
+    *out = stats;
+    stats = KernelStats();
+    return 0;
+}
+
+long long Renderer::segments() {
+    if (!allocated) return 0;
+    unsigned long long v = 0;
+    if (hipMemcpyAsync(&v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream) != hipSuccess) return -1;
+    if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+    return (long long)v;
+}
+
+int Renderer::readImage(float* host_rgb) {
+    if (!allocated) { last_error = "not allocated"; return -1; }
+    PT_HIP(hipMemcpyAsync(host_rgb, kp.image, (size_t)cfg.width * cfg.height * 3 * sizeof(float), hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipStreamSynchronize(stream));
+    return 0;
+}
+
+// Renderer::renderImage (Renderer.cpp:15-63): 54-byte BMP header, rows written
+// y = 0 (bottom) first, bytes (x, y, z) of (sum * (1/ITER)) * 255 cast to char.
+int Renderer::renderImage(const std::string& path, int iterations_total) {
+    std::vector<float> img((size_t)cfg.width * cfg.height * 3);
+    if (readImage(img.data()) != 0) return -1;
+    const int W = cfg.width, H = cfg.height;
+    unsigned char hdr[54] = {'B', 'M', 0, 0, 0, 0, 0, 0, 0, 0, 54, 0, 0, 0, 40, 0, 0, 0};
+    std::memcpy(hdr + 18, &W, 4);
+    std::memcpy(hdr + 22, &H, 4);
+    hdr[26] = 1; hdr[28] = 24;
+    const int file_size = 54 + 3 * W * H, image_size = 3 * W * H;
+    std::memcpy(hdr + 2, &file_size, 4);
+    std::memcpy(hdr + 34, &image_size, 4);
+    std::ofstream out(path, std::ios::binary);
+    if (!out) { last_error = "cannot open " + path; return -1; }
+    out.write((const char*)hdr, 54);
+    std::vector<unsigned char> row((size_t)W * 3);
+    const float div = 1 / (float)iterations_total;
+    for (int y = 0; y < H; y++) {
+        for (int x = 0; x < W; x++)
+            for (int k = 0; k < 3; k++) {
+                const float v = (img[3 * ((size_t)x + (size_t)y * W) + k] * div) * 255.0f;
+                row[3 * x + k] = (unsigned char)(f2i_x86(v) & 0xFF);
+            }
+        out.write((const char*)row.data(), (std::streamsize)row.size());
+    }
+    return out ? 0 : -1;
+}
+
+int Renderer::primaryHits(float* dist, float* normal, int* model) {
+    if (!allocated) { last_error = "not allocated"; return -1; }
+    if (!cache_valid && launchPrimary() != 0) return -1;
+    std::vector<float4> hit(kp.npix);
+    PT_HIP(hipMemcpyAsync(hit.data(), kp.cache_hit, kp.npix * sizeof(float4), hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipMemcpyAsync(model, kp.cache_model, kp.npix * sizeof(int), hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipStreamSynchronize(stream));
+    for (int i = 0; i < kp.npix; i++) {
+        dist[i] = hit[i].x;
+        normal[3 * i] = hit[i].y; normal[3 * i + 1] = hit[i].z; normal[3 * i + 2] = hit[i].w;
+    }
+    return 0;
+}
+
+int Renderer::intersectRays(int n, const float* orig, const float* dir, float* dist, float* normal, int* model) {
+    if (!allocated) { last_error = "not allocated"; return -1; }
+    if (n <= 0) return 0;
+    float *d_o, *d_d, *d_t, *d_n;
+    int* d_m;
+    PT_HIP(hipMalloc(&d_o, n * 12));
+    PT_HIP(hipMalloc(&d_d, n * 12));
+    PT_HIP(hipMalloc(&d_t, n * 4));
+    PT_HIP(hipMalloc(&d_n, n * 12));
+    PT_HIP(hipMalloc(&d_m, n * 4));
+    PT_HIP(hipMemcpyAsync(d_o, orig, n * 12, hipMemcpyHostToDevice, stream));
+    PT_HIP(hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, stream));
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL(k_intersect_rays<ACCEL_BVH>, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_t, d_n, d_m);
+    else hipLaunchKernelGGL(k_intersect_rays<ACCEL_GRID>, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_t, d_n, d_m);
+    PT_HIP(hipGetLastError());
+    PT_HIP(hipMemcpyAsync(dist, d_t, n * 4, hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipMemcpyAsync(normal, d_n, n * 12, hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipMemcpyAsync(model, d_m, n * 4, hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipStreamSynchronize(stream));
+    hipFree(d_o); hipFree(d_d); hipFree(d_t); hipFree(d_n); hipFree(d_m);
+    return 0;
+}
+
+int selftest_math(int n, const float* x, const float* y, float* out, std::string* err) {
+    if (n == 0) return 0;
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    hipError_t e = hipMalloc(&dx, n * 4);
+    if (e == hipSuccess) e = hipMalloc(&dy, n * 4);
+    if (e == hipSuccess) e = hipMalloc(&dout, (size_t)n * 20);
+    if (e == hipSuccess) e = hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dy, y, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_selftest_math, dim3((n + 255) / 256), dim3(256), 0, 0, n, dx, dy, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 20, hipMemcpyDeviceToHost);
+    hipFree(dx); hipFree(dy); hipFree(dout);
+    if (e != hipSuccess) { *err = std::string("selftest_math: ") + hipGetErrorString(e); return -1; }
+    return 0;
+}
+
+void Renderer::freeBuffers() {
+    if (stream) hipStreamSynchronize(stream);
+    for (void* p : allocs) hipFree(p);
+    allocs.clear();
+    if (!external_image) kp.image = nullptr;
+    allocated = false;
+    cache_valid = false;
+}
+
+void Renderer::free() {
+    freeBuffers();
+    for (auto& ev : bounce_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    for (auto& ev : scan_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    bounce_events.clear();
+    scan_events.clear();
+    if (own_stream && stream) hipStreamDestroy(stream);
+    stream = nullptr;
+    own_stream = false;
+}
+
+}  // namespace pt

@@ -1,0 +1,62 @@
+"""BLAS structure checks (host builder, CPU): every triangle referenced once,
+every triangle's tolerance-grown bounds inside its leaf box, depth within the
+kernels' LDS stack."""
+import numpy as np
+import pytest
+
+from conftest import REF_SCENE
+
+
+def _walk(nodes, root):
+    ints = nodes.view(np.int32)
+    leaves, depth_max = [], 0
+    stack = [(root, 1)]
+    while stack:
+        n, d = stack.pop()
+        depth_max = max(depth_max, d)
+        for c, (lo, hi, link, cnt) in enumerate([(slice(0, 3), slice(4, 7), 3, 11), (slice(8, 11), slice(12, 15), 7, 15)]):
+            count = ints[n, cnt]
+            if count < 0:
+                continue
+            box = (nodes[n, lo], nodes[n, hi])
+            if count == 0:
+                stack.append((ints[n, link], d + 1))
+            else:
+                leaves.append((ints[n, link], count, box))
+    return leaves, depth_max
+
+
+@pytest.mark.parametrize("ntri", [10, 5000, 60000])
+def test_bvh_covers_every_triangle(pt_mod, ntri):
+    from pathtracerap_amd.synthetic import torus_mesh
+    pos, nrm, tris = torus_mesh(ntri, seed=1)
+    s = pt_mod.Scene()
+    m = s.addMesh(pos, nrm, tris)
+    s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
+    s.build(bvh=True)
+    b = s.export_bvh()
+    a = s.export()
+    leaves, depth = _walk(b["nodes"], b["roots"][0])
+    assert depth <= 31
+    seen = np.zeros(len(a["tris"]), np.int32)
+    V = a["vpos"].astype(np.float64)
+    for first, cnt, (lo, hi) in leaves:
+        for t in b["refs"][first:first + cnt]:
+            seen[t] += 1
+            p = V[a["tris"][t]]
+            e1, e2 = p[1] - p[0], p[2] - p[0]
+            for u, v in ((-0.005, -0.005), (1.01, -0.005), (-0.005, 1.01)):
+                q = p[0] + u * e1 + v * e2
+                assert (q >= lo - 1e-9).all() and (q <= hi + 1e-9).all()
+    assert (seen == 1).all()
+
+
+def test_reference_scene_bvh(pt_mod):
+    s = pt_mod.Scene(REF_SCENE)
+    s.build(bvh=True)
+    b = s.export_bvh()
+    c = s.counts()
+    assert c["nbvh_refs"] == c["nt"]
+    for r in b["roots"]:
+        _, depth = _walk(b["nodes"], r)
+        assert depth <= 31
