@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X bounce loop on BASELINE.json configs[1].
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--accel bvh|grid]
+
+Workload (configs[1]): diffuse-only synthetic OBJ (~100k triangles, a
+displaced torus in an open-front room with emissive panels), 1280x1024,
+8 bounces.  One step = one sample per pixel = one full pass of the bounce
+loop (camera rays from the primary-hit cache, intersect, scatter, compact,
+accumulate) over the whole frame; the scene, ray pools and accumulator are
+resident in HBM before the timed region starts.
+
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): samples shard
+across ranks (rank r renders iterations [r*K, (r+1)*K)), then one RCCL
+all-reduce sums the float3 accumulator; weak scaling.
+
+Prints ONE JSON line (rank 0).  ``value`` = ray segments shaded per second
+over all ranks (a segment = one live ray in one bounce, primary rays
+included) in millions; ``samples_per_sec`` = pixel samples per second.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec + samples/sec at 1280×1024, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--accel", choices=["bvh", "grid"], default="bvh")
+    ap.add_argument("--ntri", type=int, default=100_000)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--metallic", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline duration")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene_path, accel_name, bounces, width, height, target_s):
+    """The oracle (C port of the reference's bounce loop) on the host cores:
+    same scene and camera, reduced resolution, 1 sample per pixel."""
+    import numpy as np
+    import oracle as O
+    import pathtracerap_amd as P
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import flat_from_export
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1))
+    s = P.Scene(scene_path)
+    s.build()
+    flat = flat_from_export(s.export())
+
+    def run(w, h):
+        cfg = O.RenderConfig(width=w, height=h, iterations=1, max_bounces=bounces, accel=0, threads=threads)
+        t = time.perf_counter()
+        _, seg = O.render(flat, cfg)
+        return seg, time.perf_counter() - t
+
+    w, h = max(8, width // 32), max(8, height // 32)
+    seg, dt = run(w, h)
+    scale = max(1.0, min(256.0, target_s / max(dt, 1e-3)))
+    f = scale ** 0.5
+    w2, h2 = min(width, int(w * f)), min(height, int(h * f))
+    if w2 > w:
+        w, h = w2, h2
+        seg, dt = run(w, h)
+    return {"value": seg / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ptoracle.c (C port of the reference renderLoop, uniform-grid accel as in "
+                      f"the reference) on the same scene/camera at {w}x{h}, 1 spp, {bounces} bounces: "
+                      f"{seg} segments in {dt:.2f}s on {threads} thread(s)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import pathtracerap_amd as P
+    from pathtracerap_amd import synthetic
+
+    tmp = tempfile.mkdtemp(prefix=f"ptbench_r{rank}_")
+    scene_path = synthetic.diffuse_scene(tmp, ntri=args.ntri, width=args.width, height=args.height,
+                                         bounces=args.bounces, accel=args.accel, metallic=args.metallic)
+    accel = P.ACCEL_BVH if args.accel == "bvh" else P.ACCEL_GRID
+    scene = P.Scene(scene_path)
+    cfg = scene.apply_settings(P.RenderConfig())
+    cfg.width, cfg.height, cfg.max_bounces, cfg.accel = args.width, args.height, args.bounces, accel
+    scene.build(grid=cfg.grid, bvh=accel == P.ACCEL_BVH)
+    ntri = scene.counts()["nt"]
+
+    image = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device=dev)
+    r = P.Renderer(cfg)
+    r.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    r.bind_image(image.data_ptr(), keepalive=image)
+    r.allocateOnGPU(scene)
+
+    K, W = args.steps, args.warmup
+    # warmup: builds the primary-hit cache, warms caches/clocks; distinct iteration ids
+    r.renderLoop(first_iter=1_000_000 + rank * max(W, 1), n_iters=W, sync=False)
+    torch.cuda.synchronize(dev)
+    r.clearImage()
+    seg0 = r.segments()
+    if not args.no_profile:
+        r.kernel_stats()          # reset
+        r.set_profiling(True)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    r.renderLoop(first_iter=rank * K, n_iters=K, sync=False)
+    if world > 1:
+        dist.all_reduce(image, op=dist.ReduceOp.SUM)      # RCCL over xGMI
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+
+    stats = r.kernel_stats() if not args.no_profile else None
+    seg = r.segments() - seg0
+    elapsed = t1 - t0
+    t = torch.tensor([elapsed, float(seg)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t[0:1].clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:2].clone(); dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, seg_total = float(tmax.item()), float(tsum.item())
+    else:
+        seg_total = float(seg)
+    img_ok = bool(torch.isfinite(image).all().item())
+    r.free()
+
+    if rank == 0:
+        npix = cfg.width * cfg.height
+        mrays = seg_total / elapsed / 1e6
+        samples = world * K * npix / elapsed
+        roof = None
+        if stats and stats["bounce_ms"] > 0:
+            P_rays = K * npix                     # primary rays (this rank)
+            # algorithmic HBM bytes of k_bounce per launch set: primary-hit cache read (20 B) +
+            # accumulator RMW (24 B) for every ray once; 48 B ray-state read + 48 B compacted
+            # write for every surviving segment (see DESIGN.md "Roofline").
+            nbytes = 44.0 * P_rays + 96.0 * (seg - P_rays)
+            per_launch_ms = stats["bounce_ms"] / max(stats["bounce_launches"], 1)
+            achieved = nbytes / (stats["bounce_ms"] / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": f"k_bounce<{args.accel}>", "bytes_per_launch": nbytes / max(stats["bounce_launches"], 1),
+                    "avg_launch_ms": round(per_launch_ms, 4), "launches": stats["bounce_launches"],
+                    "scan_ms_total": round(stats["scan_ms"], 3)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(scene_path, args.accel, args.bounces, cfg.width, cfg.height, args.cpu_seconds)
+            except Exception as e:  # noqa: BLE001 -- reported, not fatal
+                cpu = {"error": repr(e)}
+        out = {
+            "metric": METRIC, "value": round(mrays, 3), "unit": "Mrays/s", "n_gpus": world, "steps": K,
+            "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "samples_per_sec": round(samples, 1),
+            "config": {"workload": "configs[1]: diffuse-only synthetic OBJ (~100k tris), 1280x1024, 8 bounces"
+                                   + (" [metallic variant]" if args.metallic else ""),
+                       "triangles": ntri, "width": cfg.width, "height": cfg.height, "bounces": cfg.max_bounces,
+                       "spp_per_step": 1, "accel": args.accel, "parallelism": f"samples sharded x{world}",
+                       "segments": int(seg_total), "image_finite": img_ok},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

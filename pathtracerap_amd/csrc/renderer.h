@@ -91,9 +91,11 @@ private:
     KParams kp{};
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    bool stream_set = false;
     bool allocated = false;
     bool cache_valid = false;        // is_first_intersection_cached (Renderer.cpp:580)
     bool external_image = false;
+    float* ext_image = nullptr;
     bool profiling = false;
     std::vector<void*> allocs;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, scan_events;

@@ -458,15 +458,21 @@ int Renderer::fail(hipError_t e, const char* what) {
     } while (0)
 
 int Renderer::setStream(hipStream_t s) {
-    if (own_stream && stream) hipStreamDestroy(stream);
-    stream = s;
+    if (own_stream && stream) {
+        hipStreamSynchronize(stream);
+        hipStreamDestroy(stream);
+    }
+    stream = s;               // may be the null (default) stream
+    stream_set = true;
     own_stream = false;
     return 0;
 }
 
 int Renderer::bindImage(float* device_rgb) {
-    kp.image = device_rgb;
+    if (allocated && !external_image && kp.image) { last_error = "bind_image must precede allocateOnGPU"; return -1; }
+    ext_image = device_rgb;
     external_image = device_rgb != nullptr;
+    if (allocated) kp.image = device_rgb;
     return 0;
 }
 
@@ -491,7 +497,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     for (const Voxel& v : scene.voxels)
         if (v.entity_type != ENTITY_TRIANGLE) { last_error = "unsupported voxel entity type"; return -1; }
     freeBuffers();
-    if (!stream) {
+    if (!stream_set && !stream) {
         PT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         own_stream = true;
     }
@@ -526,7 +532,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &kp.ray[b][q], nullptr, cap * sizeof(float4), stream));
     PT_HIP(upload(allocs, &kp.cache_hit, nullptr, cap * sizeof(float4), stream));
     PT_HIP(upload(allocs, &kp.cache_model, nullptr, cap * sizeof(int), stream));
-    if (!external_image) PT_HIP(upload(allocs, &kp.image, nullptr, (size_t)npix_all * 3 * sizeof(float), stream));
+    if (external_image) kp.image = ext_image;
+    else PT_HIP(upload(allocs, &kp.image, nullptr, (size_t)npix_all * 3 * sizeof(float), stream));
     PT_HIP(upload(allocs, &kp.blk_cnt, nullptr, (kp.nblocks + 1) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.blk_off, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.dst_start, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
@@ -561,6 +568,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
     if (!allocated) { last_error = "renderLoop before allocateOnGPU"; return -1; }
     if (n_iters < 0 || first_iter < 0) { last_error = "bad iteration range"; return -1; }
     if (kp.npix == 0) return 0;
+    if (!kp.image || !kp.cache_hit || !kp.models) { last_error = "renderLoop: device buffers missing"; return -1; }
     if (!cache_valid) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
@@ -600,7 +608,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
 }
 
 int Renderer::synchronize() {
-    if (!stream) return 0;
+    if (!allocated && !stream) return 0;
     PT_HIP(hipStreamSynchronize(stream));
     return 0;
 }
@@ -734,10 +742,10 @@ int selftest_math(int n, const float* x, const float* y, float* out, std::string
 }
 
 void Renderer::freeBuffers() {
-    if (stream) hipStreamSynchronize(stream);
+    if (allocated || stream) hipStreamSynchronize(stream);
     for (void* p : allocs) hipFree(p);
     allocs.clear();
-    if (!external_image) kp.image = nullptr;
+    kp.image = nullptr;
     allocated = false;
     cache_valid = false;
 }
@@ -751,6 +759,7 @@ void Renderer::free() {
     if (own_stream && stream) hipStreamDestroy(stream);
     stream = nullptr;
     own_stream = false;
+    stream_set = false;
 }
 
 }  // namespace pt

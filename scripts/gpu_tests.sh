@@ -1,0 +1,7 @@
+# GPU test pass: parity tests, then the default bench line.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -25 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 16 --warmup 2 > gpurun_out/bench_bvh.json 2> gpurun_out/bench_bvh.err
+rc=$?; cat gpurun_out/bench_bvh.json; tail -5 gpurun_out/bench_bvh.err; exit $rc
