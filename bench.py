@@ -53,8 +53,8 @@ def parse():
 
 def cpu_baseline(scene_path, accel_name, bounces, width, height, target_s):
     """The oracle (C port of the reference's bounce loop) on the host cores:
-    same scene and camera, reduced resolution, 1 sample per pixel."""
-    import numpy as np
+    same scene and camera, reduced resolution, 1 sample per pixel, sized to
+    about ``target_s`` seconds of CPU work."""
     import oracle as O
     import pathtracerap_amd as P
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -65,24 +65,40 @@ def cpu_baseline(scene_path, accel_name, bounces, width, height, target_s):
     s.build()
     flat = flat_from_export(s.export())
 
-    def run(w, h):
-        cfg = O.RenderConfig(width=w, height=h, iterations=1, max_bounces=bounces, accel=0, threads=threads)
+    def run(w, h, iters):
+        cfg = O.RenderConfig(width=w, height=h, iterations=iters, max_bounces=bounces, accel=0, threads=threads)
         t = time.perf_counter()
         _, seg = O.render(flat, cfg)
         return seg, time.perf_counter() - t
 
-    w, h = max(8, width // 32), max(8, height // 32)
-    seg, dt = run(w, h)
-    scale = max(1.0, min(256.0, target_s / max(dt, 1e-3)))
-    f = scale ** 0.5
-    w2, h2 = min(width, int(w * f)), min(height, int(h * f))
-    if w2 > w:
-        w, h = w2, h2
-        seg, dt = run(w, h)
+    # probe on a 1/16-pixel frame, then size the real sample to ~target_s
+    w, h, iters = max(8, width // 4), max(8, height // 4), 1
+    seg, dt = run(w, h, iters)
+    frames = target_s / max(dt, 1e-3)          # probe-frames that fit the budget
+    if frames >= 16:
+        w, h, iters = width, height, max(1, int(frames / 16))
+    else:
+        f = max(1.0, frames) ** 0.5
+        w, h = min(width, int(w * f)), min(height, int(h * f))
+    seg, dt = run(w, h, iters)
     return {"value": seg / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ptoracle.c (C port of the reference renderLoop, uniform-grid accel as in "
-                      f"the reference) on the same scene/camera at {w}x{h}, 1 spp, {bounces} bounces: "
+                      f"the reference) on the same scene/camera at {w}x{h}, {iters} spp, {bounces} bounces: "
                       f"{seg} segments in {dt:.2f}s on {threads} thread(s)"}
+
+
+def load_pmc(kernel, workload_key):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC
+    summary (scripts/pmc_summary.py), corrected per MI355X_MICROARCH.md
+    (FETCH_SIZE x2 on gfx950, KB -> bytes); None when absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(workload_key, {}).get(kernel)
+        return None if e is None else e["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def main():
@@ -124,6 +140,7 @@ def main():
     torch.cuda.synchronize(dev)
     r.clearImage()
     seg0 = r.segments()
+    pb0 = r.segments_per_bounce()
     if not args.no_profile:
         r.kernel_stats()          # reset
         r.set_profiling(True)
@@ -142,6 +159,10 @@ def main():
 
     stats = r.kernel_stats() if not args.no_profile else None
     seg = r.segments() - seg0
+    per_bounce = [a - b for a, b in zip(r.segments_per_bounce(), pb0)]
+    while per_bounce and per_bounce[-1] == 0:
+        per_bounce.pop()
+    workload_key = f"{args.accel}_{args.ntri}_{args.width}x{args.height}_b{args.bounces}" + ("_metal" if args.metallic else "")
     elapsed = t1 - t0
     t = torch.tensor([elapsed, float(seg)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -159,18 +180,25 @@ def main():
         samples = world * K * npix / elapsed
         roof = None
         if stats and stats["bounce_ms"] > 0:
-            P_rays = K * npix                     # primary rays (this rank)
-            # algorithmic HBM bytes of k_bounce per launch set: primary-hit cache read (20 B) +
-            # accumulator RMW (24 B) for every ray once; 48 B ray-state read + 48 B compacted
-            # write for every surviving segment (see DESIGN.md "Roofline").
-            nbytes = 44.0 * P_rays + 96.0 * (seg - P_rays)
-            per_launch_ms = stats["bounce_ms"] / max(stats["bounce_launches"], 1)
+            # Dominant kernel: k_bounce<secondary> (bounces >= 1).  Algorithmic HBM bytes per ray
+            # segment entering bounce b >= 1: 48 B ray-state gather; a survivor writes 48 B of
+            # compacted state, a terminated ray read-modify-writes its 12 B accumulator pixel.
+            # Scene data (BVH nodes / triangles, ~7 MB) is cache-resident and not counted.
+            nb = [x for x in per_bounce]
+            nbytes = 0.0
+            for b in range(1, len(nb)):
+                nxt = nb[b + 1] if b + 1 < len(nb) else 0
+                nbytes += 48.0 * nb[b] + 48.0 * nxt + 24.0 * (nb[b] - nxt)
+            launches = max(stats["bounce_launches"], 1)
             achieved = nbytes / (stats["bounce_ms"] / 1e3) / 1e9
+            kname = f"k_bounce<false,{args.accel}>"
+            traffic = load_pmc(kname, workload_key)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "kernel": f"k_bounce<{args.accel}>", "bytes_per_launch": nbytes / max(stats["bounce_launches"], 1),
-                    "avg_launch_ms": round(per_launch_ms, 4), "launches": stats["bounce_launches"],
-                    "scan_ms_total": round(stats["scan_ms"], 3)}
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "kernel": kname, "algorithmic_bytes_per_launch": round(nbytes / launches),
+                    "avg_launch_ms": round(stats["bounce_ms"] / launches, 4), "launches": stats["bounce_launches"],
+                    "first_bounce_avg_ms": round(stats["first_ms"] / max(stats["first_launches"], 1), 4),
+                    "scan_avg_ms": round(stats["scan_ms"] / max(stats["scan_launches"], 1), 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -186,7 +214,8 @@ def main():
                                    + (" [metallic variant]" if args.metallic else ""),
                        "triangles": ntri, "width": cfg.width, "height": cfg.height, "bounces": cfg.max_bounces,
                        "spp_per_step": 1, "accel": args.accel, "parallelism": f"samples sharded x{world}",
-                       "segments": int(seg_total), "image_finite": img_ok},
+                       "segments": int(seg_total), "segments_per_bounce_rank0": per_bounce,
+                       "image_finite": img_ok},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

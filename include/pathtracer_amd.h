@@ -110,9 +110,12 @@ int pt_renderer_read_image(pt_renderer *r, float *host_rgb);
 int pt_renderer_render_image(pt_renderer *r, const char *bmp_path, int iterations_total);
 /* Ray segments shaded so far (sum over bounces of live rays). */
 long long pt_renderer_segments(pt_renderer *r);
+/* out[b] = live rays entering bounce b, summed over the iterations rendered (b < n, n <= 64 useful). */
+int pt_renderer_segments_per_bounce(pt_renderer *r, long long *out, int n);
 int pt_renderer_set_profiling(pt_renderer *r, int on);
-/* stats[0..4] = bounce_ms, scan_ms, primary_ms, bounce_launches, scan_launches (resets). */
-int pt_renderer_kernel_stats(pt_renderer *r, double stats[5]);
+/* stats[0..6] = secondary-bounce ms, scan ms, primary ms, secondary-bounce launches,
+ * scan launches, first-bounce ms, first-bounce launches (HIP events; resets). */
+int pt_renderer_kernel_stats(pt_renderer *r, double stats[7]);
 /* Test hooks: primary-hit cache and batch intersection (host arrays). */
 int pt_renderer_primary_hits(pt_renderer *r, float *dist, float *normal, int *model);
 int pt_renderer_intersect_rays(pt_renderer *r, int n, const float *orig, const float *dir,

@@ -90,6 +90,7 @@ EXPORTS = [
     ("pt_renderer_read_image", ctypes.c_int, [ctypes.c_void_p, _P_F]),
     ("pt_renderer_render_image", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     ("pt_renderer_segments", ctypes.c_longlong, [ctypes.c_void_p]),
+    ("pt_renderer_segments_per_bounce", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("pt_renderer_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("pt_renderer_kernel_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     ("pt_renderer_primary_hits", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_F, _P_I]),
@@ -297,14 +298,20 @@ class Renderer:
         v = lib().pt_renderer_segments(self._h)
         return _err(v, "segments")
 
+    def segments_per_bounce(self, n: int = 64) -> list:
+        out = (ctypes.c_longlong * n)()
+        _err(lib().pt_renderer_segments_per_bounce(self._h, out, n), "segments_per_bounce")
+        return list(out)
+
     def set_profiling(self, on: bool) -> None:
         _err(lib().pt_renderer_set_profiling(self._h, 1 if on else 0), "set_profiling")
 
     def kernel_stats(self) -> dict:
-        st = (ctypes.c_double * 5)()
+        st = (ctypes.c_double * 7)()
         _err(lib().pt_renderer_kernel_stats(self._h, st), "kernel_stats")
         return dict(bounce_ms=st[0], scan_ms=st[1], primary_ms=st[2],
-                    bounce_launches=int(st[3]), scan_launches=int(st[4]))
+                    bounce_launches=int(st[3]), scan_launches=int(st[4]),
+                    first_ms=st[5], first_launches=int(st[6]))
 
     def primary_hits(self):
         n = self.cfg.width * self.cfg.height

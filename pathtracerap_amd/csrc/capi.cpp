@@ -197,13 +197,18 @@ long long pt_renderer_segments(pt_renderer* r) {
     if (!r || !r->r) { set_err("null renderer"); return -1; }
     return r->r->segments();
 }
+int pt_renderer_segments_per_bounce(pt_renderer* r, long long* out, int n) {
+    if (!out || n < 0) return set_err("bad arguments");
+    R_CALL(r->r->segmentsPerBounce(out, n));
+}
 int pt_renderer_set_profiling(pt_renderer* r, int on) { R_CALL(r->r->setProfiling(on != 0)); }
-int pt_renderer_kernel_stats(pt_renderer* r, double st[5]) {
+int pt_renderer_kernel_stats(pt_renderer* r, double st[7]) {
     if (!r || !r->r || !st) return set_err("null argument");
     pt::KernelStats k;
     if (r->r->kernelStats(&k) < 0) return set_err(r->r->last_error);
     st[0] = k.bounce_ms; st[1] = k.scan_ms; st[2] = k.primary_ms;
     st[3] = (double)k.bounce_launches; st[4] = (double)k.scan_launches;
+    st[5] = k.first_ms; st[6] = (double)k.first_launches;
     return 0;
 }
 int pt_renderer_primary_hits(pt_renderer* r, float* d, float* n, int* m) {

@@ -52,12 +52,14 @@ struct KParams {
     int* blk_off;
     int* dst_start;
     int* n_live;                // live rays per bounce
-    unsigned long long* segments;
+    unsigned long long* segments;      // [0] total, [1 + b] live rays entering bounce b
 };
 
+constexpr int kMaxBounceCounters = 64;
+
 struct KernelStats {
-    double bounce_ms = 0, scan_ms = 0, primary_ms = 0;
-    long long bounce_launches = 0, scan_launches = 0;
+    double bounce_ms = 0, scan_ms = 0, primary_ms = 0, first_ms = 0;
+    long long bounce_launches = 0, scan_launches = 0, first_launches = 0;   // bounce_* = secondary bounces
 };
 
 class Renderer {
@@ -77,6 +79,7 @@ public:
     int setProfiling(bool on);
     int kernelStats(KernelStats* out);
     long long segments();
+    int segmentsPerBounce(long long* out, int n);
     int primaryHits(float* dist, float* normal, int* model);
     int intersectRays(int n, const float* orig, const float* dir, float* dist, float* normal, int* model);
 
@@ -98,7 +101,7 @@ private:
     float* ext_image = nullptr;
     bool profiling = false;
     std::vector<void*> allocs;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, scan_events;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events;
     KernelStats stats;
 };
 

@@ -411,6 +411,7 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         p.blk_off[nb] = s_part[1023];
         p.n_live[bounce + 1] = s_part[1023];
         p.segments[0] += (unsigned long long)n;
+        if (bounce < kMaxBounceCounters) p.segments[1 + bounce] += (unsigned long long)n;
     }
     __syncthreads();
     const int total = s_total;
@@ -538,8 +539,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.blk_off, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.dst_start, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.n_live, nullptr, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.segments, nullptr, sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, sizeof(unsigned long long), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (1 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (1 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -597,7 +598,11 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
                 else hipLaunchKernelGGL((k_bounce<false, ACCEL_GRID>), grid, block, 0, stream, kp, iter, b);
             }
             PT_HIP(hipGetLastError());
-            if (profiling) { hipEventRecord(e1, stream); bounce_events.push_back({e0, e1}); e0 = e1 = nullptr; }
+            if (profiling) {
+                hipEventRecord(e1, stream);
+                (b == 0 ? first_events : bounce_events).push_back({e0, e1});
+                e0 = e1 = nullptr;
+            }
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
             hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, stream, kp, b);
             PT_HIP(hipGetLastError());
@@ -627,6 +632,14 @@ int Renderer::kernelStats(KernelStats* out) {
         stats.bounce_launches++;
         hipEventDestroy(ev.first); hipEventDestroy(ev.second);
     }
+    for (auto& ev : first_events) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev.first, ev.second);
+        stats.first_ms += ms;
+        stats.first_launches++;
+        hipEventDestroy(ev.first); hipEventDestroy(ev.second);
+    }
+    first_events.clear();
     for (auto& ev : scan_events) {
         float ms = 0;
         hipEventElapsedTime(&ms, ev.first, ev.second);
@@ -647,6 +660,16 @@ long long Renderer::segments() {
     if (hipMemcpyAsync(&v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream) != hipSuccess) return -1;
     if (hipStreamSynchronize(stream) != hipSuccess) return -1;
     return (long long)v;
+}
+
+int Renderer::segmentsPerBounce(long long* out, int n) {
+    if (!allocated) { last_error = "not allocated"; return -1; }
+    unsigned long long v[1 + kMaxBounceCounters];
+    PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipStreamSynchronize(stream));
+    for (int i = 0; i < n && i < kMaxBounceCounters; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters; i < n; i++) out[i] = 0;
+    return 0;
 }
 
 int Renderer::readImage(float* host_rgb) {
@@ -753,8 +776,10 @@ void Renderer::freeBuffers() {
 void Renderer::free() {
     freeBuffers();
     for (auto& ev : bounce_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    for (auto& ev : first_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto& ev : scan_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     bounce_events.clear();
+    first_events.clear();
     scan_events.clear();
     if (own_stream && stream) hipStreamDestroy(stream);
     stream = nullptr;
