@@ -62,6 +62,7 @@ typedef struct pt_render_config {
     double cam[3];            /* camera origin (Renderer.cpp:528), default (0,0,920) */
     double plane_z;           /* image plane z (Renderer.cpp:543), default 900 */
     double plane_x0, plane_y0, plane_w, plane_h;  /* Renderer.cpp:538-542: -10,-4,20,16 */
+    int block;                /* bounce-kernel workgroup = compaction chunk: 64 (default), 128 or 256 */
 } pt_render_config;
 
 int pt_abi_version(void);

@@ -55,7 +55,7 @@ class _Cfg(ctypes.Structure):
         ("max_bounces", ctypes.c_int), ("accel", ctypes.c_int), ("grid", ctypes.c_int * 3),
         ("tail_drop", ctypes.c_int), ("cam", ctypes.c_double * 3), ("plane_z", ctypes.c_double),
         ("plane_x0", ctypes.c_double), ("plane_y0", ctypes.c_double),
-        ("plane_w", ctypes.c_double), ("plane_h", ctypes.c_double),
+        ("plane_w", ctypes.c_double), ("plane_h", ctypes.c_double), ("block", ctypes.c_int),
     ]
 
 
@@ -149,6 +149,7 @@ class RenderConfig:
     plane_y0: float = -4.0
     plane_w: float = 20.0
     plane_h: float = 16.0
+    block: int = 64
 
     def c(self) -> _Cfg:
         c = _Cfg()
@@ -159,6 +160,7 @@ class RenderConfig:
             c.cam[k] = float(self.cam[k])
         c.plane_z, c.plane_x0, c.plane_y0, c.plane_w, c.plane_h = (
             self.plane_z, self.plane_x0, self.plane_y0, self.plane_w, self.plane_h)
+        c.block = self.block
         return c
 
 

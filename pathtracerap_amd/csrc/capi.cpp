@@ -26,6 +26,7 @@ void pt_default_config(pt_render_config* c) {
     c->tail_drop = d.tail_drop;
     c->plane_z = d.plane_z; c->plane_x0 = d.plane_x0; c->plane_y0 = d.plane_y0;
     c->plane_w = d.plane_w; c->plane_h = d.plane_h;
+    c->block = d.block;
 }
 
 static pt::RenderConfig to_cfg(const pt_render_config* c) {
@@ -36,6 +37,7 @@ static pt::RenderConfig to_cfg(const pt_render_config* c) {
     d.tail_drop = c->tail_drop;
     d.plane_z = c->plane_z; d.plane_x0 = c->plane_x0; d.plane_y0 = c->plane_y0;
     d.plane_w = c->plane_w; d.plane_h = c->plane_h;
+    d.block = c->block;
     return d;
 }
 
@@ -158,6 +160,7 @@ int pt_scene_export_bvh(const pt_scene* s, float* nodes, int* refs, int* roots) 
 pt_renderer* pt_renderer_create(const pt_render_config* c) {
     if (!c) { set_err("null config"); return nullptr; }
     if (c->accel != PT_ACCEL_GRID && c->accel != PT_ACCEL_BVH) { set_err("bad accel"); return nullptr; }
+    if (c->block != 64 && c->block != 128 && c->block != 256) { set_err("block must be 64, 128 or 256"); return nullptr; }
     try {
         pt_renderer* r = new pt_renderer();
         r->r = new pt::Renderer(to_cfg(c));

@@ -19,7 +19,7 @@ enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2,
 enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1 };
 
 // One instance (Model, Primitive.h:237-244) flattened for the kernels.
-// 52 dwords; read with wave-uniform (scalar) loads inside the model loop.
+// 58 dwords; read with wave-uniform (scalar) loads inside the model loop.
 struct ModelRec {
     float w2m[12];        // world_to_model columns 0..3, rows 0..2 (m[c*3+k])
     float m2w[12];        // model_to_world, same packing
@@ -32,9 +32,10 @@ struct ModelRec {
     int tri_start, tri_end;
     int bvh_root;         // index of the mesh's BLAS root node
     float color[3];       // Material::color
+    float wbox[6];        // conservative world-space AABB of everything the instance can hit
     int pad_;
 };
-static_assert(sizeof(ModelRec) == 52 * 4, "ModelRec layout");
+static_assert(sizeof(ModelRec) == 58 * 4, "ModelRec layout");
 
 // 2-wide BVH node: both children's boxes in one 64-byte line.
 // link/count: count == 0 -> link is a child node index; count > 0 -> link is

@@ -23,6 +23,7 @@ struct RenderConfig {            // Config.h + generateRaysKernel constants, at 
     int accel = ACCEL_GRID;
     int grid[3] = {25, 25, 25};           // GRID_X/Y/Z
     int tail_drop = 0;                    // replicate ceil(n/32) launch truncation (Renderer.cpp:573)
+    int block = 64;                       // bounce-kernel workgroup size = compaction chunk (64/128/256)
     double cam[3] = {0.0, 0.0, 920.0};    // Renderer.cpp:528
     double plane_z = 900.0;               // Renderer.cpp:543
     double plane_x0 = -10.0, plane_y0 = -4.0, plane_w = 20.0, plane_h = 16.0;  // Renderer.cpp:538-542
@@ -40,8 +41,9 @@ struct KParams {
     const int* per_voxel;
     const BvhNode* bvh;
     const int* bvh_tri;
+    const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
     // frame
-    int width, height, npix, max_bounces, nblocks;
+    int width, height, npix, max_bounces, nblocks, chunk;
     float step_x, step_y, cam_x, cam_y, cam_z, plane_z;
     double plane_x0, plane_y0;
     float4* ray[2][3];          // ping-pong SoA planes: (o, pixel) (d, bounces) (color, -)
@@ -88,6 +90,7 @@ public:
 
 private:
     int launchPrimary();
+    void launchBounce(bool first, dim3 grid, int iter, int b);
     int fail(hipError_t e, const char* what);
     void freeBuffers();
 

@@ -46,27 +46,44 @@ __device__ __forceinline__ bool slab_ref(const float* bb, f3 o, f3 d, f3 inv, fl
     return true;
 }
 
-// computeRayTriangleIntersection (Renderer.cpp:174-215), edges precomputed.
-// Returns true when the test passes; *t_out is the hit distance.
-__device__ __forceinline__ bool tri_test(const float4* __restrict__ tg, int it, f3 o, f3 d, float& t_out) {
-    const float4 A = tg[3 * it + 0];
-    const float4 B = tg[3 * it + 1];
-    const float4 C = tg[3 * it + 2];
+// computeRayTriangleIntersection (Renderer.cpp:174-215) on a precomputed
+// record (v0, e1 = v1 - v0, e2 = v2 - v0).  Returns true when the reference
+// test passes; *t_out is the hit distance.  Before paying for the IEEE
+// division, u, v, u+v and t are screened against the tolerances widened from
+// 0.005 to 0.0052 using numerators scaled by |det| (no division): a test that
+// fails the screen fails the exact test too (the screen's rounding error is
+// ~1e-7 relative against a 4e-5 margin), so the exact float sequence below
+// decides every remaining case exactly as the reference does.
+__device__ __forceinline__ bool tri_test_rec(const float4 A, const float4 B, const float4 C, f3 o, f3 d, float& t_out) {
     const f3 v0 = mk3(A.x, A.y, A.z), e1 = mk3(B.x, B.y, B.z), e2 = mk3(C.x, C.y, C.z);
     f3 pvec = cross(d, e2);
     float det = dot(e1, pvec);
     if (absr(det - 0.0f) < kEps) return false;
-    float inv_det = 1 / det;
     f3 tvec = o - v0;
-    float u = dot(tvec, pvec) * inv_det;
-    if (u < 0.0f - kEps || u > 1.0f + kEps) return false;
+    const float a = dot(tvec, pvec);
+    const float sg = det > 0.0f ? 1.0f : -1.0f;
+    const float D = det * sg;
+    const float as = a * sg;
+    if (as < -0.0052f * D || as > 1.0052f * D) return false;           // u certainly out
     f3 qvec = cross(tvec, e1);
-    float v = dot(d, qvec) * inv_det;
+    const float b = dot(d, qvec);
+    const float bs = b * sg;
+    if (bs < -0.0052f * D || (as + bs) > 1.0052f * D) return false;   // v or u+v certainly out
+    const float c = dot(e2, qvec);
+    if (c * sg < -0.0052f * D) return false;                            // t certainly < -eps
+    float inv_det = 1 / det;
+    float u = a * inv_det;
+    if (u < 0.0f - kEps || u > 1.0f + kEps) return false;
+    float v = b * inv_det;
     if (v < 0.0f - kEps || u + v > 1.0f + kEps) return false;
-    float t = dot(e2, qvec) * inv_det;
+    float t = c * inv_det;
     if (t < 0.0f - kEps) return false;
     t_out = t;
     return true;
+}
+
+__device__ __forceinline__ bool tri_test(const float4* __restrict__ tg, int it, f3 o, f3 d, float& t_out) {
+    return tri_test_rec(tg[3 * it + 0], tg[3 * it + 1], tg[3 * it + 2], o, d, t_out);
 }
 
 // computeRayGridIntersection (Renderer.cpp:238-360): 3D-DDA over the model's
@@ -136,6 +153,7 @@ __device__ __forceinline__ void node_slab(const float* lo, const float* hi, f3 o
 
 // Exact closest hit over the mesh's triangles via its BLAS.  Matches the
 // brute-force scan in triangle-index order: (t, index) lexicographic minimum.
+template <int STRIDE>
 __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, float& best, int& best_tri,
                             int* __restrict__ stack) {
     bool any = false;
@@ -158,9 +176,10 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
         bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
         if (h0 && cnt0 > 0) {
             for (int i = link0; i < link0 + cnt0; i++) {
-                const int it = p.bvh_tri[i];
+                const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
+                const int it = __float_as_int(A.w);
                 float t;
-                if (tri_test(p.tri_geom, it, o, d, t)) {
+                if (tri_test_rec(A, B, C, o, d, t)) {
                     any = true;
                     if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
                 }
@@ -169,9 +188,10 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
         }
         if (h1 && cnt1 > 0) {
             for (int i = link1; i < link1 + cnt1; i++) {
-                const int it = p.bvh_tri[i];
+                const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
+                const int it = __float_as_int(A.w);
                 float t;
-                if (tri_test(p.tri_geom, it, o, d, t)) {
+                if (tri_test_rec(A, B, C, o, d, t)) {
                     any = true;
                     if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
                 }
@@ -180,7 +200,7 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
         }
         if (h0 && h1) {
             const bool first0 = tn0 <= tn1;
-            stack[sp * kBlock] = first0 ? link1 : link0;
+            stack[sp * STRIDE] = first0 ? link1 : link0;
             sp++;
             cur = first0 ? link0 : link1;
         } else if (h0) {
@@ -190,19 +210,34 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
         } else {
             if (sp == 0) break;
             sp--;
-            cur = stack[sp * kBlock];
+            cur = stack[sp * STRIDE];
         }
     }
     return any;
 }
 
 // computeRaySceneIntersectionKernel body (Renderer.cpp:364-409) for one ray.
-template <int ACCEL>
+template <int ACCEL, int STRIDE>
 __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack) {
     float gdist = kFMax;
     int gmodel = -1, gtri = -1;
+    // Instance culling against each model's conservative world box.  Exact:
+    // a culled instance either cannot pass the reference's slab test / hit a
+    // triangle, or can only hit at a world distance > gdist (and `gdist > dd`
+    // is strict).  Grid mode keeps the slab test's zero-direction quirk by
+    // never miss-culling when a model-space direction component is 0.
+    const f3 winv = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    const float dlen = sqrtf(dot(dir, dir));
     for (int im = 0; im < p.nmodels; im++) {
         const ModelRec& M = p.models[im];
+        float wtn, wtf;
+        node_slab(M.wbox, M.wbox + 3, orig, winv, wtn, wtf);
+        if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;          // cannot beat the current hit
+        if (wtn > wtf || wtf * dlen < -1.0f) {                        // misses the instance box
+            if (ACCEL != ACCEL_GRID) continue;
+            const f3 dm = xform12(M.w2m, dir, 0.0f);
+            if (dm.x != 0.0f && dm.y != 0.0f && dm.z != 0.0f) continue;
+        }
         const f3 o = xform12(M.w2m, orig, 1.0f);
         const f3 d = normalize(xform12(M.w2m, dir, 0.0f));
         const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -210,7 +245,7 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack) {
         int best_tri = -1;
         bool ok;
         if (ACCEL == ACCEL_GRID) ok = grid_closest(p, M, o, d, inv, best, best_tri);
-        else ok = bvh_closest(p, M, o, d, inv, best, best_tri, stack);
+        else ok = bvh_closest<STRIDE>(p, M, o, d, inv, best, best_tri, stack);
         if (ok) {
             const f3 nd = normalize(d);
             const f3 pm = o + nd * best;
@@ -291,7 +326,7 @@ __global__ __launch_bounds__(kBlock) void k_primary(KParams p) {
     if (i >= p.npix) return;
     f3 o, d;
     camera_ray(p, i, o, d);
-    const Hit h = intersect_scene<ACCEL>(p, o, d, s_stack + threadIdx.x);
+    const Hit h = intersect_scene<ACCEL, kBlock>(p, o, d, s_stack + threadIdx.x);
     p.cache_hit[i] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
     p.cache_model[i] = h.model;
 }
@@ -303,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
     __shared__ int s_stack[ACCEL == ACCEL_BVH ? kStack * kBlock : 1];
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const Hit h = intersect_scene<ACCEL>(p, mk3(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]),
+    const Hit h = intersect_scene<ACCEL, kBlock>(p, mk3(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]),
                                          mk3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), s_stack + threadIdx.x);
     dist[i] = h.dist;
     nrm[3 * i] = h.n.x; nrm[3 * i + 1] = h.n.y; nrm[3 * i + 2] = h.n.z;
@@ -311,12 +346,12 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
 }
 
 // One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
-template <bool FIRST, int ACCEL>
-__global__ __launch_bounds__(kBlock) void k_bounce(KParams p, int iter, int bounce) {
-    __shared__ int s_stack[(!FIRST && ACCEL == ACCEL_BVH) ? kStack * kBlock : 1];
-    __shared__ int s_wave[kBlock / 64];
+template <bool FIRST, int ACCEL, int BS>
+__global__ __launch_bounds__(BS) void k_bounce(KParams p, int iter, int bounce) {
+    __shared__ int s_stack[(!FIRST && ACCEL == ACCEL_BVH) ? kStack * BS : 1];
+    __shared__ int s_wave[BS / 64];
     const int n = FIRST ? p.npix : p.n_live[bounce];
-    const int j0 = blockIdx.x * kBlock;
+    const int j0 = blockIdx.x * BS;
     if (j0 >= n) return;                       // whole block idle (uniform)
     const int j = j0 + threadIdx.x;
     const bool active = j < n;
@@ -341,14 +376,14 @@ __global__ __launch_bounds__(kBlock) void k_bounce(KParams p, int iter, int boun
                 const int mid = (lo + hi + 1) >> 1;
                 if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
             }
-            const int src = lo * kBlock + (j - p.blk_off[lo]);
+            const int src = lo * BS + (j - p.blk_off[lo]);
             const float4 a = p.ray[in_buf][0][src];
             const float4 b = p.ray[in_buf][1][src];
             const float4 c = p.ray[in_buf][2][src];
             r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
             r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
             r.c = mk3(c.x, c.y, c.z);
-            h = intersect_scene<ACCEL>(p, r.o, r.d, s_stack + threadIdx.x);
+            h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x);
         }
         shade(p, r, h, iter, j);
     }
@@ -365,11 +400,15 @@ __global__ __launch_bounds__(kBlock) void k_bounce(KParams p, int iter, int boun
     const unsigned long long m = __ballot(alive);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int rank = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_wave[wid] = __popcll(m);
-    __syncthreads();
     int base = 0, total = 0;
+    if (BS > 64) {
+        if (lane == 0) s_wave[wid] = __popcll(m);
+        __syncthreads();
+    } else {
+        total = __popcll(m);
+    }
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; w++) {
+    for (int w = 0; w < (BS > 64 ? BS / 64 : 0); w++) {
         const int c = s_wave[w];
         base += (w < wid) ? c : 0;
         total += c;
@@ -391,7 +430,8 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
     __shared__ int s_total;
     const int tid = threadIdx.x;
     const int n = bounce == 0 ? p.npix : p.n_live[bounce];
-    const int nb = (n + kBlock - 1) / kBlock;
+    const int CH = p.chunk;
+    const int nb = (n + CH - 1) / CH;
     const int per = (nb + 1023) / 1024;
     const int s = tid * per, e = min(s + per, nb);
     int sum = 0;
@@ -419,9 +459,9 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         const int c = p.blk_cnt[i];
         if (c == 0) continue;
         const int o0 = p.blk_off[i];
-        for (int bd = (o0 + kBlock - 1) / kBlock; bd * kBlock < o0 + c; bd++) p.dst_start[bd] = i;
+        for (int bd = (o0 + CH - 1) / CH; bd * CH < o0 + c; bd++) p.dst_start[bd] = i;
     }
-    if (tid == 0) p.dst_start[(total + kBlock - 1) / kBlock] = nb > 0 ? nb - 1 : 0;
+    if (tid == 0) p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
 }
 
 __global__ void k_selftest_math(int n, const float* x, const float* y, float* out) {
@@ -515,20 +555,22 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.per_voxel, scene.per_voxel_data_pool.data(), scene.per_voxel_data_pool.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
 
     kp.width = cfg.width;
     kp.height = cfg.height;
     const int npix_all = cfg.width * cfg.height;
     kp.npix = cfg.tail_drop ? (npix_all / 32) * 32 : npix_all;
     kp.max_bounces = cfg.max_bounces;
-    kp.nblocks = (npix_all + kBlock - 1) / kBlock;
+    kp.chunk = (cfg.block == 64 || cfg.block == 128 || cfg.block == 256) ? cfg.block : 256;
+    kp.nblocks = (npix_all + kp.chunk - 1) / kp.chunk;
     kp.step_x = (float)(cfg.plane_w / cfg.width);
     kp.step_y = (float)(cfg.plane_h / cfg.height);
     kp.cam_x = (float)cfg.cam[0]; kp.cam_y = (float)cfg.cam[1]; kp.cam_z = (float)cfg.cam[2];
     kp.plane_z = (float)cfg.plane_z;
     kp.plane_x0 = cfg.plane_x0;
     kp.plane_y0 = cfg.plane_y0;
-    const size_t cap = (size_t)kp.nblocks * kBlock;
+    const size_t cap = (size_t)kp.nblocks * kp.chunk;
     for (int b = 0; b < 2; b++)
         for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &kp.ray[b][q], nullptr, cap * sizeof(float4), stream));
     PT_HIP(upload(allocs, &kp.cache_hit, nullptr, cap * sizeof(float4), stream));
@@ -565,6 +607,29 @@ int Renderer::launchPrimary() {
     return 0;
 }
 
+template <bool FIRST, int BS>
+static void launch_bounce_bs(int accel, dim3 grid, hipStream_t st, const KParams& kp, int iter, int b) {
+    if (accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_BVH, BS>), grid, dim3(BS), 0, st, kp, iter, b);
+    else hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_GRID, BS>), grid, dim3(BS), 0, st, kp, iter, b);
+}
+
+void Renderer::launchBounce(bool first, dim3 grid, int iter, int b) {
+    switch (kp.chunk) {
+        case 64:
+            if (first) launch_bounce_bs<true, 64>(cfg.accel, grid, stream, kp, iter, b);
+            else launch_bounce_bs<false, 64>(cfg.accel, grid, stream, kp, iter, b);
+            break;
+        case 128:
+            if (first) launch_bounce_bs<true, 128>(cfg.accel, grid, stream, kp, iter, b);
+            else launch_bounce_bs<false, 128>(cfg.accel, grid, stream, kp, iter, b);
+            break;
+        default:
+            if (first) launch_bounce_bs<true, 256>(cfg.accel, grid, stream, kp, iter, b);
+            else launch_bounce_bs<false, 256>(cfg.accel, grid, stream, kp, iter, b);
+            break;
+    }
+}
+
 int Renderer::renderLoop(int first_iter, int n_iters) {
     if (!allocated) { last_error = "renderLoop before allocateOnGPU"; return -1; }
     if (n_iters < 0 || first_iter < 0) { last_error = "bad iteration range"; return -1; }
@@ -583,20 +648,14 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             hipEventDestroy(e0); hipEventDestroy(e1);
         }
     }
-    const dim3 grid((unsigned)kp.nblocks), block(kBlock);
+    const dim3 grid((unsigned)kp.nblocks);
     const int passes = cfg.max_bounces > 1 ? cfg.max_bounces : 1;
     for (int it = 0; it < n_iters; it++) {
         const int iter = first_iter + it;
         for (int b = 0; b < passes; b++) {
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
-            if (b == 0) {
-                if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<true, ACCEL_BVH>), grid, block, 0, stream, kp, iter, b);
-                else hipLaunchKernelGGL((k_bounce<true, ACCEL_GRID>), grid, block, 0, stream, kp, iter, b);
-            } else {
-                if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<false, ACCEL_BVH>), grid, block, 0, stream, kp, iter, b);
-                else hipLaunchKernelGGL((k_bounce<false, ACCEL_GRID>), grid, block, 0, stream, kp, iter, b);
-            }
+            launchBounce(b == 0, grid, iter, b);
             PT_HIP(hipGetLastError());
             if (profiling) {
                 hipEventRecord(e1, stream);

@@ -566,6 +566,12 @@ void Scene::buildDeviceTables() {
         float* q = &tri_normal[t * 4];
         q[0] = n.x; q[1] = n.y; q[2] = n.z; q[3] = 0.0f;
     }
+    bvh_tri_geom.assign(bvh_tri_order.size() * 12, 0.0f);
+    for (size_t i = 0; i < bvh_tri_order.size(); i++) {
+        const int t = bvh_tri_order[i];
+        std::memcpy(&bvh_tri_geom[i * 12], &tri_geom[(size_t)t * 12], 12 * sizeof(float));
+        std::memcpy(&bvh_tri_geom[i * 12 + 3], &t, sizeof(int));
+    }
     model_recs.resize(models.size());
     for (size_t i = 0; i < models.size(); i++) {
         const Model& m = models[i];
@@ -590,6 +596,48 @@ void Scene::buildDeviceTables() {
         r.tri_end = mesh.triangle_indices.end_index;
         r.bvh_root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m.mesh_index];
         for (int k = 0; k < 3; k++) r.color[k] = m.mat.color[k];
+        world_box(m, mesh, r.bvh_root, r.wbox);
+    }
+}
+
+// Conservative world AABB of an instance (instance culling in the kernels):
+// the mesh bbox and, when built, the BLAS root's (tolerance-grown, padded)
+// child boxes, grown by 1e-3 of the diagonal, mapped through model_to_world in
+// double and padded again.  A ray that misses it cannot pass the reference's
+// slab test nor hit any triangle of the instance.
+void Scene::world_box(const Model& m, const Mesh& mesh, int root, float* out) const {
+    double lo[3] = {mesh.bounding_box.min.x, mesh.bounding_box.min.y, mesh.bounding_box.min.z};
+    double hi[3] = {mesh.bounding_box.max.x, mesh.bounding_box.max.y, mesh.bounding_box.max.z};
+    if (root >= 0 && root < (int)bvh_nodes.size()) {
+        const BvhNode& n = bvh_nodes[root];
+        if (n.count0 >= 0)
+            for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], (double)n.lo0[k]); hi[k] = std::max(hi[k], (double)n.hi0[k]); }
+        if (n.count1 >= 0)
+            for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], (double)n.lo1[k]); hi[k] = std::max(hi[k], (double)n.hi1[k]); }
+    }
+    double diag = 0;
+    for (int k = 0; k < 3; k++) diag += (hi[k] - lo[k]) * (hi[k] - lo[k]);
+    diag = std::sqrt(std::max(diag, 0.0));
+    const double pad = 1e-3 * diag + 1.0;
+    double wlo[3] = {1e300, 1e300, 1e300}, whi[3] = {-1e300, -1e300, -1e300};
+    bool finite = std::isfinite(diag);
+    for (int c = 0; c < 8; c++) {
+        const double p[3] = {(c & 1) ? hi[0] + pad : lo[0] - pad, (c & 2) ? hi[1] + pad : lo[1] - pad,
+                             (c & 4) ? hi[2] + pad : lo[2] - pad};
+        for (int k = 0; k < 3; k++) {
+            const double w = (double)m.model_to_world[0 * 4 + k] * p[0] + (double)m.model_to_world[1 * 4 + k] * p[1] +
+                             (double)m.model_to_world[2 * 4 + k] * p[2] + (double)m.model_to_world[3 * 4 + k];
+            finite &= std::isfinite(w);
+            wlo[k] = std::min(wlo[k], w);
+            whi[k] = std::max(whi[k], w);
+        }
+    }
+    double wd = 0;
+    for (int k = 0; k < 3; k++) wd += (whi[k] - wlo[k]) * (whi[k] - wlo[k]);
+    const double wpad = 1e-4 * std::sqrt(std::max(wd, 0.0)) + 1e-2;
+    for (int k = 0; k < 3; k++) {
+        out[k] = finite ? (float)(wlo[k] - wpad) : -3e38f;
+        out[3 + k] = finite ? (float)(whi[k] + wpad) : 3e38f;
     }
 }
 

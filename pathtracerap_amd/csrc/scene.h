@@ -87,6 +87,7 @@ public:
     std::vector<ModelRec> model_recs;
     std::vector<BvhNode> bvh_nodes;   // all meshes' BLAS, concatenated
     std::vector<int> bvh_tri_order;   // leaf triangle references (global triangle index)
+    std::vector<float> bvh_tri_geom;  // 12 floats / leaf reference: tri_geom in leaf order, v0.w = index bits
     std::vector<int> mesh_bvh_root;
 
     RenderSettings settings;          // optional RENDER block of the config
@@ -98,6 +99,7 @@ private:
     void addMeshesToGrid();
     void buildDeviceTables();
     void buildBvh(int mesh);
+    void world_box(const Model& m, const Mesh& mesh, int root, float* out) const;
 };
 
 // glm restatements (Scene.cpp:30-39): M = T * R * S, W = inverse(M).

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""In-process A/B of renderer variants on the bench workload (interleaved
+rounds on one device; cdna_hip_programming.md §5.4 rule 24).
+
+    python scripts/ab.py --variants bvh:256 bvh:128 bvh:64 grid:256 --rounds 5 --steps 8
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", nargs="+", default=["bvh:256", "bvh:128", "bvh:64"])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--ntri", type=int, default=100_000)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--scene", default=None, help="scene file instead of the synthetic one")
+    a = ap.parse_args()
+    import torch
+    import pathtracerap_amd as P
+    from pathtracerap_amd import synthetic
+    path = a.scene or synthetic.diffuse_scene(tempfile.mkdtemp(), ntri=a.ntri)
+    scenes = {}
+    rs = {}
+    for v in a.variants:
+        accel, block = v.split(":")
+        acc = P.ACCEL_BVH if accel == "bvh" else P.ACCEL_GRID
+        if acc not in scenes:
+            s = P.Scene(path)
+            s.build(bvh=acc == P.ACCEL_BVH)
+            scenes[acc] = s
+        cfg = P.RenderConfig(width=a.width, height=a.height, max_bounces=a.bounces, accel=acc, block=int(block))
+        r = P.Renderer(cfg)
+        r.allocateOnGPU(scenes[acc])
+        r.renderLoop(1000, 2)          # warm + primary cache
+        rs[v] = r
+    times = {v: [] for v in a.variants}
+    segs = {}
+    for rnd in range(a.rounds):
+        for v, r in rs.items():
+            s0 = r.segments()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r.renderLoop(rnd * a.steps, a.steps)
+            times[v].append((time.perf_counter() - t) / a.steps * 1e3)
+            segs[v] = (r.segments() - s0) / a.steps
+    out = {}
+    for v in a.variants:
+        med = statistics.median(times[v])
+        out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
+                  "Mrays_s": round(segs[v] / med / 1e3, 1)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
