@@ -601,19 +601,31 @@ void Scene::buildDeviceTables() {
 }
 
 // Conservative world AABB of an instance (instance culling in the kernels):
-// the mesh bbox and, when built, the BLAS root's (tolerance-grown, padded)
-// child boxes, grown by 1e-3 of the diagonal, mapped through model_to_world in
-// double and padded again.  A ray that misses it cannot pass the reference's
-// slab test nor hit any triangle of the instance.
+// the mesh bbox united with every triangle grown by the reference test's
+// barycentric tolerances (all points the test can accept), grown by 1e-3 of
+// the diagonal, mapped through model_to_world in double and padded again.  A
+// ray that misses it cannot pass the reference's slab test, and no hit the
+// test accepts lies outside it.
 void Scene::world_box(const Model& m, const Mesh& mesh, int root, float* out) const {
+    (void)root;
     double lo[3] = {mesh.bounding_box.min.x, mesh.bounding_box.min.y, mesh.bounding_box.min.z};
     double hi[3] = {mesh.bounding_box.max.x, mesh.bounding_box.max.y, mesh.bounding_box.max.z};
-    if (root >= 0 && root < (int)bvh_nodes.size()) {
-        const BvhNode& n = bvh_nodes[root];
-        if (n.count0 >= 0)
-            for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], (double)n.lo0[k]); hi[k] = std::max(hi[k], (double)n.hi0[k]); }
-        if (n.count1 >= 0)
-            for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], (double)n.lo1[k]); hi[k] = std::max(hi[k], (double)n.hi1[k]); }
+    // every point the reference triangle test can accept: u >= -e, v >= -e, u + v <= 1 + e
+    const double e = (double)kEps;
+    const double uv[3][2] = {{-e, -e}, {1 + 2 * e, -e}, {-e, 1 + 2 * e}};
+    for (int t = mesh.triangle_indices.start_index; t < mesh.triangle_indices.end_index; t++) {
+        const f3 a = vertices[triangles[t].vertex_indices[0]].position;
+        const f3 b = vertices[triangles[t].vertex_indices[1]].position;
+        const f3 c = vertices[triangles[t].vertex_indices[2]].position;
+        const double v0[3] = {a.x, a.y, a.z};
+        const double e1[3] = {(double)b.x - a.x, (double)b.y - a.y, (double)b.z - a.z};
+        const double e2[3] = {(double)c.x - a.x, (double)c.y - a.y, (double)c.z - a.z};
+        for (int q = 0; q < 3; q++)
+            for (int k = 0; k < 3; k++) {
+                const double pk = v0[k] + uv[q][0] * e1[k] + uv[q][1] * e2[k];
+                lo[k] = std::min(lo[k], pk);
+                hi[k] = std::max(hi[k], pk);
+            }
     }
     double diag = 0;
     for (int k = 0; k < 3; k++) diag += (hi[k] - lo[k]) * (hi[k] - lo[k]);

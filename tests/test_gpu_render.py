@@ -137,12 +137,14 @@ def _random_rays(n, seed, center=(0.0, 100.0, 0.0), spread=600.0):
 
 @pytest.mark.parametrize("accel", [0, 1])
 def test_intersect_random_rays_reference_scene(gpu, pt_mod, oracle_mod, accel):
+    """400k rays from inside the room (origins on and near walls, grazing the
+    huge wall triangles' tolerance regions) + axis-aligned directions."""
     P, O = pt_mod, oracle_mod
     s = P.Scene(REF_SCENE)
     s.build(bvh=accel == 1)
     r = P.Renderer(P.RenderConfig(width=8, height=8, accel=accel))
     r.allocateOnGPU(s)
-    o, d = _random_rays(20000, 11)
+    o, d = _random_rays(400000, 11, center=(25.0, 380.0, 0.0), spread=480.0)
     t, n, m = r.intersect_rays(o, d)
     r.free()
     ot, on, om = O.intersect_rays(flat_from_export(s.export()), o, d, accel=accel)
