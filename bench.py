@@ -3,6 +3,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--accel bvh|grid]
 
+Default mode ``grid_fast`` returns the reference algorithm's results bit for
+bit (uniform-grid semantics computed through a BVH hit set); the exact
+closest-hit ``bvh`` mode is timed after it and reported under ``alt_mode``.
+
 Workload (configs[1]): diffuse-only synthetic OBJ (~100k triangles, a
 displaced torus in an open-front room with emissive panels), 1280x1024,
 8 bounces.  One step = one sample per pixel = one full pass of the bounce
@@ -39,7 +43,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--accel", choices=["bvh", "grid"], default="bvh")
+    ap.add_argument("--accel", choices=["bvh", "grid", "grid_fast"], default="grid_fast",
+                    help="grid_fast: the reference's grid results (bit-identical), BVH-accelerated; "
+                         "bvh: exact closest hit; grid: the reference's list-walking DDA")
+    ap.add_argument("--alt-accel", default="bvh", help="second mode timed after the main one ('' to skip)")
     ap.add_argument("--ntri", type=int, default=100_000)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=1024)
@@ -121,11 +128,11 @@ def main():
     tmp = tempfile.mkdtemp(prefix=f"ptbench_r{rank}_")
     scene_path = synthetic.diffuse_scene(tmp, ntri=args.ntri, width=args.width, height=args.height,
                                          bounces=args.bounces, accel=args.accel, metallic=args.metallic)
-    accel = P.ACCEL_BVH if args.accel == "bvh" else P.ACCEL_GRID
+    accel = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[args.accel]
     scene = P.Scene(scene_path)
     cfg = scene.apply_settings(P.RenderConfig())
     cfg.width, cfg.height, cfg.max_bounces, cfg.accel = args.width, args.height, args.bounces, accel
-    scene.build(grid=cfg.grid, bvh=accel == P.ACCEL_BVH)
+    scene.build(grid=cfg.grid, bvh=accel != P.ACCEL_GRID)
     ntri = scene.counts()["nt"]
 
     image = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device=dev)
@@ -174,6 +181,42 @@ def main():
     img_ok = bool(torch.isfinite(image).all().item())
     r.free()
 
+    alt = None
+    if args.alt_accel and args.alt_accel != args.accel:
+        acc2 = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[args.alt_accel]
+        cfg2 = P.RenderConfig(width=cfg.width, height=cfg.height, max_bounces=cfg.max_bounces, accel=acc2,
+                              grid=cfg.grid, block=cfg.block)
+        if acc2 != P.ACCEL_GRID and accel == P.ACCEL_GRID:
+            scene.build(grid=cfg.grid, bvh=True)
+        r2 = P.Renderer(cfg2)
+        r2.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        r2.bind_image(image.data_ptr(), keepalive=image)
+        r2.allocateOnGPU(scene)
+        r2.renderLoop(first_iter=2_000_000 + rank * max(W, 1), n_iters=W, sync=False)
+        torch.cuda.synchronize(dev)
+        s2 = r2.segments()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        a0 = time.perf_counter()
+        r2.renderLoop(first_iter=rank * K, n_iters=K, sync=False)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        a1 = time.perf_counter()
+        seg2 = float(r2.segments() - s2)
+        r2.free()
+        ta = torch.tensor([a1 - a0, seg2], dtype=torch.float64, device=dev)
+        if world > 1:
+            tm = ta[0:1].clone(); dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            ts = ta[1:2].clone(); dist.all_reduce(ts, op=dist.ReduceOp.SUM)
+            ta = torch.cat([tm, ts])
+        alt = {"accel": args.alt_accel, "value": round(float(ta[1]) / float(ta[0]) / 1e6, 3), "unit": "Mrays/s",
+               "ms_per_step": round(float(ta[0]) / K * 1e3, 3),
+               "samples_per_sec": round(world * K * cfg.width * cfg.height / float(ta[0]), 1),
+               "semantics": "exact closest hit (statistically equivalent image, not per-pixel identical)"
+               if args.alt_accel == "bvh" else "reference grid (bit-identical)"}
+
     if rank == 0:
         npix = cfg.width * cfg.height
         mrays = seg_total / elapsed / 1e6
@@ -213,10 +256,13 @@ def main():
             "config": {"workload": "configs[1]: diffuse-only synthetic OBJ (~100k tris), 1280x1024, 8 bounces"
                                    + (" [metallic variant]" if args.metallic else ""),
                        "triangles": ntri, "width": cfg.width, "height": cfg.height, "bounces": cfg.max_bounces,
-                       "spp_per_step": 1, "accel": args.accel, "parallelism": f"samples sharded x{world}",
+                       "spp_per_step": 1, "accel": args.accel,
+                       "results": "bit-identical to the reference algorithm (oracle-checked)"
+                       if args.accel != "bvh" else "exact closest hit",
+                       "parallelism": f"samples sharded x{world}",
                        "segments": int(seg_total), "segments_per_bounce_rank0": per_bounce,
                        "image_finite": img_ok},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "alt_mode": alt,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -45,8 +45,9 @@ enum {
 
 /* Intersect-stage acceleration structure. */
 enum {
-    PT_ACCEL_GRID = 0,   /* reference uniform grid + DDA (Renderer.cpp:238-360), bit-exact */
-    PT_ACCEL_BVH = 1     /* MI355X BVH, exact closest hit with the reference triangle test */
+    PT_ACCEL_GRID = 0,      /* reference uniform grid + DDA (Renderer.cpp:238-360), bit-exact */
+    PT_ACCEL_BVH = 1,       /* MI355X BVH, exact closest hit with the reference triangle test */
+    PT_ACCEL_GRID_FAST = 2  /* PT_ACCEL_GRID's result via BVH hit set + voxel-box DDA walk (needs BVH) */
 };
 
 typedef struct pt_scene pt_scene;

@@ -24,13 +24,14 @@ from dataclasses import dataclass, field
 import numpy as np
 
 __all__ = ["Scene", "Renderer", "RenderConfig", "PathTracerError", "build", "lib",
-           "MATERIALS", "ACCEL_GRID", "ACCEL_BVH"]
+           "MATERIALS", "ACCEL_GRID", "ACCEL_BVH", "ACCEL_GRID_FAST"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libpathtracer_amd.so")
 
 ACCEL_GRID = 0
 ACCEL_BVH = 1
+ACCEL_GRID_FAST = 2
 # Primitive.h:213-222
 MATERIALS = {"DIFFUSE": 0, "SPECULAR": 1, "REFLECTIVE": 2, "REFRACTIVE": 3,
              "EMISSIVE": 4, "COAT": 5, "METAL": 6}

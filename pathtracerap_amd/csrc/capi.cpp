@@ -159,7 +159,10 @@ int pt_scene_export_bvh(const pt_scene* s, float* nodes, int* refs, int* roots) 
 
 pt_renderer* pt_renderer_create(const pt_render_config* c) {
     if (!c) { set_err("null config"); return nullptr; }
-    if (c->accel != PT_ACCEL_GRID && c->accel != PT_ACCEL_BVH) { set_err("bad accel"); return nullptr; }
+    if (c->accel != PT_ACCEL_GRID && c->accel != PT_ACCEL_BVH && c->accel != PT_ACCEL_GRID_FAST) {
+        set_err("bad accel");
+        return nullptr;
+    }
     if (c->block != 64 && c->block != 128 && c->block != 256) { set_err("block must be 64, 128 or 256"); return nullptr; }
     try {
         pt_renderer* r = new pt_renderer();
@@ -242,7 +245,7 @@ int pt_render(const char* scene_config, const pt_render_config* cfg, const char*
     if (!s) return -1;
     int rc = pt_scene_load_config(s, scene_config);
     if (rc >= 0) rc = pt_scene_apply_settings(s, &c);
-    if (rc >= 0) rc = pt_scene_build(s, c.grid, c.accel == PT_ACCEL_BVH);
+    if (rc >= 0) rc = pt_scene_build(s, c.grid, c.accel != PT_ACCEL_GRID);
     pt_renderer* r = rc >= 0 ? pt_renderer_create(&c) : nullptr;
     if (rc >= 0 && !r) rc = -1;
     if (rc >= 0) rc = pt_renderer_allocate_on_gpu(r, s);

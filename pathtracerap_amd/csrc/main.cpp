@@ -11,7 +11,7 @@
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s scene.txt [out.bmp] [--res W H] [--iter N] [--bounces B] [--bvh]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s scene.txt [out.bmp] [--res W H] [--iter N] [--bounces B] [--bvh|--grid-fast]\n", argv[0]);
         return 2;
     }
     pt_render_config cfg;
@@ -25,9 +25,10 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--iter") && i + 1 < argc) cfg.iterations = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--bounces") && i + 1 < argc) cfg.max_bounces = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--bvh")) cfg.accel = PT_ACCEL_BVH;
+        else if (!std::strcmp(argv[i], "--grid-fast")) cfg.accel = PT_ACCEL_GRID_FAST;
         else out = argv[i];
     }
-    if (pt_scene_build(s, cfg.grid, cfg.accel == PT_ACCEL_BVH) < 0) { std::fprintf(stderr, "%s\n", pt_last_error()); return 1; }
+    if (pt_scene_build(s, cfg.grid, cfg.accel != PT_ACCEL_GRID) < 0) { std::fprintf(stderr, "%s\n", pt_last_error()); return 1; }
     pt_renderer* r = pt_renderer_create(&cfg);
     if (!r || pt_renderer_allocate_on_gpu(r, s) < 0) { std::fprintf(stderr, "%s\n", pt_last_error()); return 1; }
     auto t0 = std::chrono::high_resolution_clock::now();

@@ -16,7 +16,12 @@ enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2,
 //              exact closest hit with the reference's triangle test; equals
 //              the grid result except where the grid's early exit misses a
 //              nearer triangle.
-enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1 };
+//  ACCEL_GRID_FAST: the ACCEL_GRID result computed without voxel triangle
+//              lists: the BLAS collects the ray's hit set H (every triangle the
+//              reference test accepts), then the reference DDA walks the grid
+//              testing only voxel-box membership of H.  Bit-identical to
+//              ACCEL_GRID; needs the BVH.
+enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1, ACCEL_GRID_FAST = 2 };
 
 // One instance (Model, Primitive.h:237-244) flattened for the kernels.
 // 58 dwords; read with wave-uniform (scalar) loads inside the model loop.
@@ -33,7 +38,7 @@ struct ModelRec {
     int bvh_root;         // index of the mesh's BLAS root node
     float color[3];       // Material::color
     float wbox[6];        // conservative world-space AABB of everything the instance can hit
-    int pad_;
+    float reach;          // R: max triangle bbox diagonal + 3 voxel diagonals (+ slack), model units
 };
 static_assert(sizeof(ModelRec) == 58 * 4, "ModelRec layout");
 

@@ -54,7 +54,8 @@ struct KParams {
     int* blk_off;
     int* dst_start;
     int* n_live;                // live rays per bounce
-    unsigned long long* segments;      // [0] total, [1 + b] live rays entering bounce b
+    unsigned long long* segments;      // [0] total, [1 + b] live rays entering bounce b, [65] diagnostics
+    int debug;                          // timing-only ablation switches (PT_DEBUG_ABLATE); 0 in production
 };
 
 constexpr int kMaxBounceCounters = 64;

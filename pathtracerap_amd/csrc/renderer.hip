@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 
@@ -216,9 +217,225 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     return any;
 }
 
-// computeRaySceneIntersectionKernel body (Renderer.cpp:364-409) for one ray.
+constexpr int kHitCap = 8;   // hit-set capacity per lane (LDS); overflow -> exact list-walking DDA
+
+// BLAS traversal collecting hit-set members: triangles the reference test
+// accepts, as (t bits, index, packed voxel box lo, hi) in the lane's LDS slots
+// hs[i * STRIDE].  BOUNDED: only members with t <= t_min + 2R are required
+// (nodes entered beyond that are pruned; extra members are harmless).
+// Returns the count (-1 on overflow); *tmin_out = smallest t accepted.
+template <int STRIDE, bool BOUNDED>
+__device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, int* __restrict__ stack,
+                           int4* __restrict__ hs, float* tmin_out) {
+    int nh = 0;
+    float tmin = kFMax;
+    const float margin = 2.0f * M.reach;
+    int sp = 0;
+    int cur = M.bvh_root;
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+    for (;;) {
+        const float4 q0 = nodes[4 * cur + 0];
+        const float4 q1 = nodes[4 * cur + 1];
+        const float4 q2 = nodes[4 * cur + 2];
+        const float4 q3 = nodes[4 * cur + 3];
+        const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+        const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+        const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+        const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+        float tn0, tf0, tn1, tf1;
+        node_slab(lo0, hi0, o, inv, tn0, tf0);
+        node_slab(lo1, hi1, o, inv, tn1, tf1);
+        const float bound = BOUNDED ? tmin + margin : 3.0e38f;
+        bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bound;
+        bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bound;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const bool hc = c == 0 ? h0 : h1;
+            const int cc = c == 0 ? cnt0 : cnt1;
+            const int lc = c == 0 ? link0 : link1;
+            if (hc && cc > 0) {
+                for (int i = lc; i < lc + cc; i++) {
+                    const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
+                    float t;
+                    if (!tri_test_rec(A, B, C, o, d, t)) continue;
+                    if (BOUNDED) {
+                        if (t < tmin) tmin = t;
+                        if (t > tmin + margin) continue;          // not required (NaN is kept)
+                        if (nh == kHitCap) {                       // drop members now beyond the bound
+                            int w = 0;
+                            for (int q = 0; q < nh; q++) {
+                                const int4 e = hs[q * STRIDE];
+                                if (!(__int_as_float(e.x) > tmin + margin)) hs[(w++) * STRIDE] = e;
+                            }
+                            nh = w;
+                        }
+                    } else if (t < tmin) {
+                        tmin = t;
+                    }
+                    if (nh == kHitCap) return -1;
+                    hs[nh * STRIDE] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
+                                                __float_as_int(C.w));
+                    nh++;
+                }
+            }
+        }
+        if (cnt0 > 0) h0 = false;
+        if (cnt1 > 0) h1 = false;
+        if (h0 && h1) {
+            const bool first0 = tn0 <= tn1;                         // near child first tightens the bound
+            stack[sp * STRIDE] = first0 ? link1 : link0;
+            sp++;
+            cur = first0 ? link0 : link1;
+        } else if (h0) {
+            cur = link0;
+        } else if (h1) {
+            cur = link1;
+        } else {
+            if (sp == 0) break;
+            sp--;
+            cur = stack[sp * STRIDE];
+        }
+    }
+    *tmin_out = tmin;
+    return nh;
+}
+
+__device__ __forceinline__ bool vbox_has(int lo, int hi, int ix, int iy, int iz) {
+    return ix >= (lo & 1023) && ix <= (hi & 1023) && iy >= ((lo >> 10) & 1023) && iy <= ((hi >> 10) & 1023) &&
+           iz >= ((lo >> 20) & 1023) && iz <= ((hi >> 20) & 1023);
+}
+
+struct WalkResult {
+    bool hit;        // computeRayGridIntersection's return value
+    float t;         // winning member's t (valid when has_best)
+    int tri;
+    bool has_best;
+    bool final_min;  // a member with t == tmin was tested: the result is final
+    float tw;        // ray parameter (from the model-space origin) where the walk stopped
+};
+
+// The reference's DDA walk (Renderer.cpp:263-358) over M's grid, with voxel
+// triangle lists replaced by the hit set: voxel V holds triangle h in its list
+// iff V lies in h's voxel box (Scene.cpp:364-374), and h's test outcome does not
+// depend on V, so V is a hit voxel iff some member's box contains V.  The
+// reference keeps the first strict minimum in test order (voxel order, then
+// ascending index inside a list): the lexicographic minimum of (t, step, index).
+template <int STRIDE>
+__device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
+                                  const int4* __restrict__ hs, int nh, float tmin) {
+    const int GX = p.gdim[0], GY = p.gdim[1], GZ = p.gdim[2];
+    int ix = f2i_sat(absr(pt.x - M.bbox[0] + kEps) / M.vw[0]);
+    int iy = f2i_sat(absr(pt.y - M.bbox[1] + kEps) / M.vw[1]);
+    int iz = f2i_sat(absr(pt.z - M.bbox[2] + kEps) / M.vw[2]);
+    ix = ix < 0 ? 0 : (ix > GX - 1 ? GX - 1 : ix);
+    iy = iy < 0 ? 0 : (iy > GY - 1 ? GY - 1 : iy);
+    iz = iz < 0 ? 0 : (iz > GZ - 1 ? GZ - 1 : iz);
+    f3 tmax = mk3(kFMax, kFMax, kFMax), delta = mk3(kFMax, kFMax, kFMax);
+    const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
+    const int ox = d.x > 0.0f ? GX : -1, oy = d.y > 0.0f ? GY : -1, oz = d.z > 0.0f ? GZ : -1;
+    const int nx = d.x > 0.0f ? ix + 1 : ix, ny = d.y > 0.0f ? iy + 1 : iy, nz = d.z > 0.0f ? iz + 1 : iz;
+    const float px = M.bbox[0] + (float)nx * M.vw[0];
+    const float py = M.bbox[1] + (float)ny * M.vw[1];
+    const float pz = M.bbox[2] + (float)nz * M.vw[2];
+    if (d.x != 0) { delta.x = absr(M.vw[0] * inv.x); tmax.x = (px - pt.x) * inv.x; }
+    if (d.y != 0) { delta.y = absr(M.vw[1] * inv.y); tmax.y = (py - pt.y) * inv.y; }
+    if (d.z != 0) { delta.z = absr(M.vw[2] * inv.z); tmax.z = (pz - pt.z) * inv.z; }
+    // union of the members' voxel boxes: outside it no voxel is a hit voxel
+    int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
+    for (int h = 0; h < nh; h++) {
+        const int4 e = hs[h * STRIDE];
+        ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
+        uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
+    }
+    const unsigned all = (1u << nh) - 1u;
+    int cx = 0, cy = 0, cz = 0;
+    bool hit = false;
+    unsigned tested = 0;
+    float bt = kFMax;
+    int bk = -1, bi = -1;
+    for (int k = 0;; k++) {
+        bool vhit = false;
+        if (ix >= ulx && ix <= uhx && iy >= uly && iy <= uhy && iz >= ulz && iz <= uhz) {
+            for (int h = 0; h < nh; h++) {
+                const int4 e = hs[h * STRIDE];
+                if (vbox_has(e.z, e.w, ix, iy, iz)) {
+                    vhit = true;
+                    if (!((tested >> h) & 1u)) {
+                        tested |= 1u << h;
+                        const float t = __int_as_float(e.x);
+                        if (t < bt || (t == bt && (k < bk || (k == bk && e.y < bi)))) { bt = t; bk = k; bi = e.y; }
+                    }
+                }
+            }
+        }
+        if (vhit) { cx = ix; cy = iy; cz = iz; hit = true; }
+        // Exact shortcuts: once a minimum-t member (or every member) is tested the
+        // result and the return value are final; once the monotone walk has passed
+        // the union box along an axis it enters no member's box again.
+        if (tested == all || (bk >= 0 && bt == tmin)) break;
+        if ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz)) break;
+        if (hit && (iabs(cx - ix) > 2 || iabs(cy - iy) > 2 || iabs(cz - iz) > 2)) break;
+        if (tmax.x < tmax.y && tmax.x < tmax.z) {
+            ix += sx;
+            if (ix == ox || tmax.x >= kFMax) break;
+            tmax.x += delta.x;
+        } else if (tmax.y < tmax.z) {
+            iy += sy;
+            if (iy == oy || tmax.y >= kFMax) break;
+            tmax.y += delta.y;
+        } else {
+            iz += sz;
+            if (iz == oz || tmax.z >= kFMax) break;
+            tmax.z += delta.z;
+        }
+    }
+    WalkResult w;
+    w.hit = hit;
+    w.t = bt;
+    w.tri = bi;
+    w.has_best = bk >= 0;
+    w.final_min = bk >= 0 && bt == tmin;
+    w.tw = t_box + fminf(fminf(tmax.x, tmax.y), tmax.z);
+    return w;
+}
+
+// computeRayGridIntersection (Renderer.cpp:238-360), result-identical, via the
+// BLAS hit set and hitset_walk.
+// Tier 1 collects members with t <= t_min + 2R only (R = ModelRec::reach: a
+// member whose voxel box the walk enters at parameter tau has t <= tau + R).
+// It is exact when the walk tests a minimum-t member (every box entered before
+// that belongs to a member with t <= t_min + 2R) or stops before parameter
+// t_min + R (no uncollected member's box is reachable).  Otherwise tier 2
+// collects the whole set; on hit-set overflow the list-walking DDA runs.
+template <int STRIDE>
+__device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, float& best, int& best_tri,
+                            int* __restrict__ stack, int4* __restrict__ hs) {
+    float t_box;
+    if (!slab_ref(M.bbox, o, d, inv, t_box)) return false;
+    const f3 pt = o + d * t_box;
+    if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) return false;
+    if (p.debug & 2) return bvh_closest<STRIDE>(p, M, o, d, inv, best, best_tri, stack);   // timing-only ablation
+    float tmin;
+    int nh = bvh_collect<STRIDE, true>(p, M, o, d, inv, stack, hs, &tmin);
+    if (nh == 0) return false;           // no accepted triangle anywhere on the ray: no hit voxel
+    WalkResult w;
+    bool done = false;
+    if (nh > 0) {
+        w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
+        done = w.final_min || w.tw < tmin + M.reach;
+    }
+    if (!done) {
+        if (p.debug & 4) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);   // tier-2 counter (diagnostic)
+        nh = bvh_collect<STRIDE, false>(p, M, o, d, inv, stack, hs, &tmin);
+        if (nh < 0) return grid_closest(p, M, o, d, inv, best, best_tri);   // overflow: exact slow path
+        w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
+    }
+    if (w.hit && w.has_best) { best = w.t; best_tri = w.tri; }
+    return w.hit;
+}
+
 template <int ACCEL, int STRIDE>
-__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack) {
+__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs) {
     float gdist = kFMax;
     int gmodel = -1, gtri = -1;
     // Instance culling against each model's conservative world box.  Exact:
@@ -234,7 +451,7 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack) {
         node_slab(M.wbox, M.wbox + 3, orig, winv, wtn, wtf);
         if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;          // cannot beat the current hit
         if (wtn > wtf || wtf * dlen < -1.0f) {                        // misses the instance box
-            if (ACCEL != ACCEL_GRID) continue;
+            if (ACCEL == ACCEL_BVH) continue;
             const f3 dm = xform12(M.w2m, dir, 0.0f);
             if (dm.x != 0.0f && dm.y != 0.0f && dm.z != 0.0f) continue;
         }
@@ -245,6 +462,7 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack) {
         int best_tri = -1;
         bool ok;
         if (ACCEL == ACCEL_GRID) ok = grid_closest(p, M, o, d, inv, best, best_tri);
+        else if (ACCEL == ACCEL_GRID_FAST) ok = grid_hitset<STRIDE>(p, M, o, d, inv, best, best_tri, stack, hs);
         else ok = bvh_closest<STRIDE>(p, M, o, d, inv, best, best_tri, stack);
         if (ok) {
             const f3 nd = normalize(d);
@@ -321,12 +539,13 @@ __device__ __forceinline__ void shade(const KParams& p, RayState& r, const Hit& 
 // Primary intersections, cached once per renderer (Renderer.cpp:596-613).
 template <int ACCEL>
 __global__ __launch_bounds__(kBlock) void k_primary(KParams p) {
-    __shared__ int s_stack[ACCEL == ACCEL_BVH ? kStack * kBlock : 1];
+    __shared__ int s_stack[ACCEL != ACCEL_GRID ? kStack * kBlock : 1];
+    __shared__ int4 s_hs[ACCEL == ACCEL_GRID_FAST ? kHitCap * kBlock : 1];
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= p.npix) return;
     f3 o, d;
     camera_ray(p, i, o, d);
-    const Hit h = intersect_scene<ACCEL, kBlock>(p, o, d, s_stack + threadIdx.x);
+    const Hit h = intersect_scene<ACCEL, kBlock>(p, o, d, s_stack + threadIdx.x, s_hs + threadIdx.x);
     p.cache_hit[i] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
     p.cache_model[i] = h.model;
 }
@@ -335,11 +554,13 @@ __global__ __launch_bounds__(kBlock) void k_primary(KParams p) {
 template <int ACCEL>
 __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, const float* orig, const float* dir,
                                                            float* dist, float* nrm, int* model) {
-    __shared__ int s_stack[ACCEL == ACCEL_BVH ? kStack * kBlock : 1];
+    __shared__ int s_stack[ACCEL != ACCEL_GRID ? kStack * kBlock : 1];
+    __shared__ int4 s_hs[ACCEL == ACCEL_GRID_FAST ? kHitCap * kBlock : 1];
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const Hit h = intersect_scene<ACCEL, kBlock>(p, mk3(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]),
-                                         mk3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), s_stack + threadIdx.x);
+                                         mk3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), s_stack + threadIdx.x,
+                                         s_hs + threadIdx.x);
     dist[i] = h.dist;
     nrm[3 * i] = h.n.x; nrm[3 * i + 1] = h.n.y; nrm[3 * i + 2] = h.n.z;
     model[i] = h.model;
@@ -348,7 +569,8 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
 // One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
 template <bool FIRST, int ACCEL, int BS>
 __global__ __launch_bounds__(BS) void k_bounce(KParams p, int iter, int bounce) {
-    __shared__ int s_stack[(!FIRST && ACCEL == ACCEL_BVH) ? kStack * BS : 1];
+    __shared__ int s_stack[(!FIRST && ACCEL != ACCEL_GRID) ? kStack * BS : 1];
+    __shared__ int4 s_hs[(!FIRST && ACCEL == ACCEL_GRID_FAST) ? kHitCap * BS : 1];
     __shared__ int s_wave[BS / 64];
     const int n = FIRST ? p.npix : p.n_live[bounce];
     const int j0 = blockIdx.x * BS;
@@ -383,7 +605,7 @@ __global__ __launch_bounds__(BS) void k_bounce(KParams p, int iter, int bounce) 
             r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
             r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
             r.c = mk3(c.x, c.y, c.z);
-            h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x);
+            h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
         }
         shade(p, r, h, iter, j);
     }
@@ -534,7 +756,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     if ((long long)cfg.width * cfg.height > (1LL << 30)) { last_error = "resolution too large"; return -1; }
     for (int k = 0; k < 3; k++)
         if (cfg.grid[k] != scene.grid_dim[k]) { last_error = "config grid dims differ from the scene build"; return -1; }
-    if (cfg.accel == ACCEL_BVH && scene.bvh_nodes.empty()) { last_error = "scene built without BVH"; return -1; }
+    if (cfg.accel != ACCEL_GRID && scene.bvh_nodes.empty()) { last_error = "scene built without BVH"; return -1; }
     for (const Voxel& v : scene.voxels)
         if (v.entity_type != ENTITY_TRIANGLE) { last_error = "unsupported voxel entity type"; return -1; }
     freeBuffers();
@@ -562,6 +784,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     const int npix_all = cfg.width * cfg.height;
     kp.npix = cfg.tail_drop ? (npix_all / 32) * 32 : npix_all;
     kp.max_bounces = cfg.max_bounces;
+    {
+        const char* dbg = std::getenv("PT_DEBUG_ABLATE");   // timing-only ablations; results become wrong
+        kp.debug = dbg ? std::atoi(dbg) : 0;
+    }
     kp.chunk = (cfg.block == 64 || cfg.block == 128 || cfg.block == 256) ? cfg.block : 256;
     kp.nblocks = (npix_all + kp.chunk - 1) / kp.chunk;
     kp.step_x = (float)(cfg.plane_w / cfg.width);
@@ -581,8 +807,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.blk_off, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.dst_start, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.n_live, nullptr, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.segments, nullptr, (1 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, (1 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (2 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (2 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -601,6 +827,7 @@ int Renderer::clearImage() {
 int Renderer::launchPrimary() {
     const dim3 grid((unsigned)((kp.npix + kBlock - 1) / kBlock));
     if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL(k_primary<ACCEL_BVH>, grid, dim3(kBlock), 0, stream, kp);
+    else if (cfg.accel == ACCEL_GRID_FAST) hipLaunchKernelGGL(k_primary<ACCEL_GRID_FAST>, grid, dim3(kBlock), 0, stream, kp);
     else hipLaunchKernelGGL(k_primary<ACCEL_GRID>, grid, dim3(kBlock), 0, stream, kp);
     PT_HIP(hipGetLastError());
     cache_valid = true;
@@ -610,6 +837,8 @@ int Renderer::launchPrimary() {
 template <bool FIRST, int BS>
 static void launch_bounce_bs(int accel, dim3 grid, hipStream_t st, const KParams& kp, int iter, int b) {
     if (accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_BVH, BS>), grid, dim3(BS), 0, st, kp, iter, b);
+    else if (accel == ACCEL_GRID_FAST)
+        hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_GRID_FAST, BS>), grid, dim3(BS), 0, st, kp, iter, b);
     else hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_GRID, BS>), grid, dim3(BS), 0, st, kp, iter, b);
 }
 
@@ -723,11 +952,11 @@ long long Renderer::segments() {
 
 int Renderer::segmentsPerBounce(long long* out, int n) {
     if (!allocated) { last_error = "not allocated"; return -1; }
-    unsigned long long v[1 + kMaxBounceCounters];
+    unsigned long long v[2 + kMaxBounceCounters];
     PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n && i < kMaxBounceCounters; i++) out[i] = (long long)v[1 + i];
-    for (int i = kMaxBounceCounters; i < n; i++) out[i] = 0;
+    for (int i = 0; i < n && i < kMaxBounceCounters + 1; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters + 1; i < n; i++) out[i] = 0;
     return 0;
 }
 
@@ -795,6 +1024,8 @@ int Renderer::intersectRays(int n, const float* orig, const float* dir, float* d
     PT_HIP(hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, stream));
     const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
     if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL(k_intersect_rays<ACCEL_BVH>, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_t, d_n, d_m);
+    else if (cfg.accel == ACCEL_GRID_FAST)
+        hipLaunchKernelGGL(k_intersect_rays<ACCEL_GRID_FAST>, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_t, d_n, d_m);
     else hipLaunchKernelGGL(k_intersect_rays<ACCEL_GRID>, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_t, d_n, d_m);
     PT_HIP(hipGetLastError());
     PT_HIP(hipMemcpyAsync(dist, d_t, n * 4, hipMemcpyDeviceToHost, stream));

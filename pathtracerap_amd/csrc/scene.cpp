@@ -424,7 +424,8 @@ int Scene::loadConfig(const std::string& path) {
                 else if (key == "grid" && parse_vec(val, v) && v.size() == 3) {
                     for (int k = 0; k < 3; k++) settings.grid[k] = (int)v[k];
                 } else if (key == "accel") {
-                    settings.accel = (val == "bvh") ? ACCEL_BVH : ACCEL_GRID; settings.has_accel = true;
+                    settings.accel = (val == "bvh") ? ACCEL_BVH : (val == "grid_fast") ? ACCEL_GRID_FAST : ACCEL_GRID;
+                    settings.has_accel = true;
                 } else return fail("bad RENDER line " + b[i]);
             }
             continue;
@@ -498,6 +499,7 @@ void Scene::addMeshesToGrid() {
     grids.clear();
     voxels.clear();
     per_voxel_data_pool.clear();
+    tri_vbox.assign(triangles.size() * 2, 0);
     const int GX = grid_dim[0], GY = grid_dim[1], GZ = grid_dim[2];
     std::vector<bool> is_mesh_processed(meshes.size(), false);
     std::vector<int> grid_index_cache(meshes.size(), 0);
@@ -529,6 +531,9 @@ void Scene::addMeshesToGrid() {
                 mn[a] = mn[a] < 0 ? 0 : (mn[a] > gd[a] - 1 ? gd[a] - 1 : mn[a]);
                 mx[a] = mx[a] < 0 ? 0 : (mx[a] > gd[a] - 1 ? gd[a] - 1 : mx[a]);
             }
+            // the voxel box [mn, mx] is exactly the set of voxels whose list holds t
+            tri_vbox[2 * (size_t)t] = mn[0] | (mn[1] << 10) | (mn[2] << 20);
+            tri_vbox[2 * (size_t)t + 1] = mx[0] | (mx[1] << 10) | (mx[2] << 20);
             for (int z = mn[2]; z <= mx[2]; z++)
                 for (int y = mn[1]; y <= mx[1]; y++)
                     for (int x = mn[0]; x <= mx[0]; x++) buf[(size_t)x + (size_t)y * GX + (size_t)GX * GY * z].push_back(t);
@@ -571,6 +576,8 @@ void Scene::buildDeviceTables() {
         const int t = bvh_tri_order[i];
         std::memcpy(&bvh_tri_geom[i * 12], &tri_geom[(size_t)t * 12], 12 * sizeof(float));
         std::memcpy(&bvh_tri_geom[i * 12 + 3], &t, sizeof(int));
+        std::memcpy(&bvh_tri_geom[i * 12 + 7], &tri_vbox[2 * (size_t)t], sizeof(int));
+        std::memcpy(&bvh_tri_geom[i * 12 + 11], &tri_vbox[2 * (size_t)t + 1], sizeof(int));
     }
     model_recs.resize(models.size());
     for (size_t i = 0; i < models.size(); i++) {
@@ -597,6 +604,19 @@ void Scene::buildDeviceTables() {
         r.bvh_root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m.mesh_index];
         for (int k = 0; k < 3; k++) r.color[k] = m.mat.color[k];
         world_box(m, mesh, r.bvh_root, r.wbox);
+        // Bounded hit-set collection (ACCEL_GRID_FAST): a triangle whose voxel box the
+        // DDA enters at ray parameter tau has its hit within tau + R.
+        double tmax_diag = 0;
+        for (int t = mesh.triangle_indices.start_index; t < mesh.triangle_indices.end_index; t++) {
+            BoundingBox tb;
+            for (int j = 0; j < 3; j++) tb.update(vertices[triangles[t].vertex_indices[j]].position);
+            const double dx = (double)tb.max.x - tb.min.x, dy = (double)tb.max.y - tb.min.y, dz = (double)tb.max.z - tb.min.z;
+            tmax_diag = std::max(tmax_diag, std::sqrt(dx * dx + dy * dy + dz * dz));
+        }
+        const double vd = std::sqrt((double)g.voxel_width[0] * g.voxel_width[0] + (double)g.voxel_width[1] * g.voxel_width[1] +
+                                    (double)g.voxel_width[2] * g.voxel_width[2]);
+        const double R = 1.02 * (1.02 * tmax_diag + 3.0 * vd) + 1.0;
+        r.reach = std::isfinite(R) ? (float)R : 3e38f;
     }
 }
 

@@ -87,7 +87,9 @@ public:
     std::vector<ModelRec> model_recs;
     std::vector<BvhNode> bvh_nodes;   // all meshes' BLAS, concatenated
     std::vector<int> bvh_tri_order;   // leaf triangle references (global triangle index)
-    std::vector<float> bvh_tri_geom;  // 12 floats / leaf reference: tri_geom in leaf order, v0.w = index bits
+    std::vector<float> bvh_tri_geom;  // 12 floats / leaf reference: tri_geom in leaf order; w lanes carry
+                                      // the triangle index and its packed grid voxel box (mn, mx; 10 bits/axis)
+    std::vector<int> tri_vbox;        // 2 ints / triangle: packed computeVoxelIndex min / max
     std::vector<int> mesh_bvh_root;
 
     RenderSettings settings;          // optional RENDER block of the config

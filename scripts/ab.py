@@ -35,10 +35,10 @@ def main():
     rs = {}
     for v in a.variants:
         accel, block = v.split(":")
-        acc = P.ACCEL_BVH if accel == "bvh" else P.ACCEL_GRID
+        acc = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[accel]
         if acc not in scenes:
             s = P.Scene(path)
-            s.build(bvh=acc == P.ACCEL_BVH)
+            s.build(bvh=acc != P.ACCEL_GRID)
             scenes[acc] = s
         cfg = P.RenderConfig(width=a.width, height=a.height, max_bounces=a.bounces, accel=acc, block=int(block))
         r = P.Renderer(cfg)
@@ -60,6 +60,9 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
+        diag = rs[v].segments_per_bounce(65)[64]
+        if diag:
+            out[v]["diag_counter"] = diag
     print(json.dumps(out, indent=1))
 
 

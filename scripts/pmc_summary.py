@@ -19,10 +19,12 @@ import sys
 from collections import defaultdict
 
 KERNELS = {
-    "k_bounce<false, 1>": "k_bounce<false,bvh>",
-    "k_bounce<false, 0>": "k_bounce<false,grid>",
-    "k_bounce<true, 1>": "k_bounce<true,bvh>",
-    "k_bounce<true, 0>": "k_bounce<true,grid>",
+    "k_bounce<false, 2,": "k_bounce<false,grid_fast>",
+    "k_bounce<true, 2,": "k_bounce<true,grid_fast>",
+    "k_bounce<false, 1,": "k_bounce<false,bvh>",
+    "k_bounce<false, 0,": "k_bounce<false,grid>",
+    "k_bounce<true, 1,": "k_bounce<true,bvh>",
+    "k_bounce<true, 0,": "k_bounce<true,grid>",
     "k_scan": "k_scan",
 }
 

@@ -13,9 +13,15 @@ def flat_from_export(a: dict, gdim=(25, 25, 25)) -> "O.FlatScene":
 
 def oracle_cfg(cfg, threads=1) -> "O.RenderConfig":
     return O.RenderConfig(width=cfg.width, height=cfg.height, iterations=cfg.iterations, first_iter=0,
-                          max_bounces=cfg.max_bounces, accel=cfg.accel, threads=threads, tail_drop=cfg.tail_drop,
+                          max_bounces=cfg.max_bounces, accel=oracle_accel(cfg.accel), threads=threads, tail_drop=cfg.tail_drop,
                           cam=tuple(cfg.cam), plane_z=cfg.plane_z, plane_x0=cfg.plane_x0, plane_y0=cfg.plane_y0,
                           plane_w=cfg.plane_w, plane_h=cfg.plane_h)
+
+
+def oracle_accel(accel):
+    """GPU accel -> oracle semantics: GRID (0) and GRID_FAST (2) are the
+    reference grid; BVH (1) is the exact closest hit."""
+    return 1 if accel == 1 else 0
 
 
 def bits(a):

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 def _render_bmp_payload(P, accel, tmp_path):
     s = P.Scene(REF_SCENE)
-    s.build(bvh=accel == 1)
+    s.build(bvh=accel != 0)
     cfg = s.apply_settings(P.RenderConfig())
     cfg.accel = accel
     assert (cfg.width, cfg.height, cfg.iterations, cfg.max_bounces) == (1000, 800, 500, 5)
@@ -41,8 +41,9 @@ def _stats(a, b):
     return (d == 0).mean(), (d <= 1).mean(), (d <= 2).mean(), d.max()
 
 
-def test_grid_full_size_equals_oracle_and_reference(gpu, pt_mod, tmp_path):
-    px, seg = _render_bmp_payload(pt_mod, 0, tmp_path)
+@pytest.mark.parametrize("accel", [0, 2])
+def test_grid_full_size_equals_oracle_and_reference(gpu, pt_mod, tmp_path, accel):
+    px, seg = _render_bmp_payload(pt_mod, accel, tmp_path)
     oracle_px = np.load(os.path.join(GOLDEN, "oracle_render_1000x800_500.npz"))["bgr"]
     assert seg == 1293177856
     assert np.array_equal(px, oracle_px), "GPU 500-iteration render differs from the pinned oracle render"

@@ -20,10 +20,10 @@ def _ref_scene(P, bvh=False):
     return s
 
 
-@pytest.mark.parametrize("accel", [0, 1])
+@pytest.mark.parametrize("accel", [0, 1, 2])
 def test_primary_hits_bitexact(gpu, pt_mod, oracle_mod, accel):
     P, O = pt_mod, oracle_mod
-    s = _ref_scene(P, bvh=accel == 1)
+    s = _ref_scene(P, bvh=accel != 0)
     cfg = P.RenderConfig(width=160, height=128, iterations=1, accel=accel)
     r = P.Renderer(cfg)
     r.allocateOnGPU(s)
@@ -36,10 +36,10 @@ def test_primary_hits_bitexact(gpu, pt_mod, oracle_mod, accel):
     assert_bitexact(n[hit], on[hit], "normal")
 
 
-@pytest.mark.parametrize("accel", [0, 1])
+@pytest.mark.parametrize("accel", [0, 1, 2])
 def test_render_reference_scene_bitexact(gpu, pt_mod, oracle_mod, accel):
     P, O = pt_mod, oracle_mod
-    s = _ref_scene(P, bvh=accel == 1)
+    s = _ref_scene(P, bvh=accel != 0)
     cfg = P.RenderConfig(width=200, height=160, iterations=3, accel=accel)
     r = P.Renderer(cfg)
     r.allocateOnGPU(s)

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from conftest import REF_SCENE
-from helpers import assert_bitexact, flat_from_export, oracle_cfg
+from helpers import assert_bitexact, flat_from_export, oracle_accel, oracle_cfg
 
 pytestmark = pytest.mark.gpu
 
@@ -41,14 +41,14 @@ def test_device_math_bitexact(gpu, pt_mod, oracle_mod):
     assert_bitexact(out, want, "device math")
 
 
-@pytest.mark.parametrize("accel", [0, 1])
+@pytest.mark.parametrize("accel", [0, 1, 2])
 @pytest.mark.parametrize("metallic", [False, True])
 def test_synthetic_scene_bitexact(gpu, pt_mod, oracle_mod, synth_dir, accel, metallic):
     from pathtracerap_amd import synthetic
     P, O = pt_mod, oracle_mod
     path = synthetic.diffuse_scene(synth_dir, ntri=3000, seed=2, metallic=metallic)
     s = P.Scene(path)
-    s.build(bvh=accel == 1)
+    s.build(bvh=accel != 0)
     cfg = P.RenderConfig(width=96, height=72, iterations=2, max_bounces=8, accel=accel)
     img, seg, oimg, oseg = _render_both(P, O, s, cfg)
     assert seg == oseg
@@ -135,19 +135,19 @@ def _random_rays(n, seed, center=(0.0, 100.0, 0.0), spread=600.0):
     return o, d
 
 
-@pytest.mark.parametrize("accel", [0, 1])
+@pytest.mark.parametrize("accel", [0, 1, 2])
 def test_intersect_random_rays_reference_scene(gpu, pt_mod, oracle_mod, accel):
     """400k rays from inside the room (origins on and near walls, grazing the
     huge wall triangles' tolerance regions) + axis-aligned directions."""
     P, O = pt_mod, oracle_mod
     s = P.Scene(REF_SCENE)
-    s.build(bvh=accel == 1)
+    s.build(bvh=accel != 0)
     r = P.Renderer(P.RenderConfig(width=8, height=8, accel=accel))
     r.allocateOnGPU(s)
     o, d = _random_rays(400000, 11, center=(25.0, 380.0, 0.0), spread=480.0)
     t, n, m = r.intersect_rays(o, d)
     r.free()
-    ot, on, om = O.intersect_rays(flat_from_export(s.export()), o, d, accel=accel)
+    ot, on, om = O.intersect_rays(flat_from_export(s.export()), o, d, accel=oracle_accel(accel))
     assert (om >= 0).mean() > 0.3
     assert_bitexact(m, om, "model")
     assert_bitexact(t, ot, "dist")
@@ -198,3 +198,42 @@ def test_bmp_bytes_match_oracle_writer(gpu, pt_mod, oracle_mod, tmp_path):
     img = r.image()
     r.free()
     assert out.read_bytes() == O.to_bmp_bytes(img, 64, 48, 3)
+
+
+def _comb_mesh(nplanes=20, gap=0.05):
+    """nplanes parallel unit quads stacked along z: rays along z cross all of
+    them, overflowing the fast grid's 8-entry hit set."""
+    P_, N_, T_ = [], [], []
+    for k in range(nplanes):
+        z = k * gap
+        b = len(P_)
+        P_ += [(-1, -1, z), (1, -1, z), (1, 1, z), (-1, 1, z)]
+        N_ += [(0, 0, 1)] * 4
+        T_ += [(b, b + 1, b + 2), (b, b + 2, b + 3)]
+    return np.array(P_, np.float32), np.array(N_, np.float32), np.array(T_, np.int32)
+
+
+@pytest.mark.parametrize("accel", [0, 2])
+def test_grid_fast_hitset_overflow_falls_back_exactly(gpu, pt_mod, oracle_mod, accel):
+    P, O = pt_mod, oracle_mod
+    pos, nrm, tris = _comb_mesh()
+    s = P.Scene()
+    m = s.addMesh(pos, nrm, tris)
+    s.addModel(m, (0.1, 0.1, 0.1), (0, 10, 5), (0, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.addModel(m, (0.05, 0.05, 0.05), (80, 0, 0), (30, 20, -10), "METAL", (0.5, 0.5, 0.5))
+    s.build(bvh=True)
+    r = P.Renderer(P.RenderConfig(width=8, height=8, accel=accel))
+    r.allocateOnGPU(s)
+    rs = np.random.RandomState(9)
+    n = 20000
+    o = np.c_[rs.uniform(-120, 120, (n, 2)), np.full(n, 300.0)].astype(np.float32)
+    d = np.c_[rs.normal(size=(n, 2)) * 0.05, -np.ones(n)].astype(np.float32)
+    o2, d2 = _random_rays(20000, 4, center=(0, 0, 0), spread=200)
+    o, d = np.concatenate([o, o2]), np.concatenate([d, d2])
+    t, nn, mm = r.intersect_rays(o, d)
+    r.free()
+    ot, on, om = O.intersect_rays(flat_from_export(s.export()), o, d, accel=0)
+    assert (om >= 0).mean() > 0.2
+    assert_bitexact(mm, om, "model")
+    assert_bitexact(t, ot, "dist")
+    assert_bitexact(nn[om >= 0], on[om >= 0], "normal")
