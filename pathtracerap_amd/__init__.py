@@ -27,7 +27,7 @@ __all__ = ["Scene", "Renderer", "RenderConfig", "PathTracerError", "build", "lib
            "MATERIALS", "ACCEL_GRID", "ACCEL_BVH", "ACCEL_GRID_FAST"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libpathtracer_amd.so")
+_LIB_PATH = os.environ.get("PT_LIB_PATH") or os.path.join(_HERE, "libpathtracer_amd.so")   # override: experiments
 
 ACCEL_GRID = 0
 ACCEL_BVH = 1

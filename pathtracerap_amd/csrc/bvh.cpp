@@ -5,7 +5,8 @@
 // triangle grown by its u/v tolerances (EPSILON = 0.005 in barycentric
 // units) plus a float-rounding pad -- so traversal never prunes a triangle
 // the brute-force closest-hit oracle would pick.  Depth is capped at
-// kMaxDepth so the kernels' fixed LDS traversal stack cannot overflow.
+// kMaxDepth (balanced splits once the budget gets tight, a larger leaf at the
+// cap) so the kernels' fixed LDS traversal stack cannot overflow.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -19,7 +20,7 @@ namespace {
 
 constexpr int kLeafMax = 4;
 constexpr int kBins = 16;
-constexpr int kMaxDepth = 30;   // kernel stack holds kMaxDepth + 2 entries
+constexpr int kMaxDepth = 23;   // <= the kernels' LDS stack (PT_STACK = 24 entries)
 
 struct Box {
     double lo[3] = {1e300, 1e300, 1e300};
@@ -63,7 +64,7 @@ struct Builder {
         Box box, cbox;
         for (int i = b; i < e; i++) { box.grow(refs[i].box); cbox.grow(refs[i].c); }
         const int n = e - b;
-        if (n <= kLeafMax) return leaf(b, e, box);
+        if (n <= kLeafMax || depth >= kMaxDepth) return leaf(b, e, box);   // depth cap: a (rare) larger leaf
         // Force balanced splits when the remaining depth budget is tight.
         const bool force_median = depth + ceil_log2((n + kLeafMax - 1) / kLeafMax) >= kMaxDepth - 1;
         int axis = 0;

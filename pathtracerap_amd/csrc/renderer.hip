@@ -25,7 +25,16 @@
 namespace pt {
 
 constexpr int kBlock = 256;
-constexpr int kStack = 32;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
+#ifndef PT_STACK
+#define PT_STACK 24
+#endif
+#ifndef PT_HITCAP
+#define PT_HITCAP 6
+#endif
+#ifndef PT_MINWAVES
+#define PT_MINWAVES 5
+#endif
+constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
 
 // ---------------------------------------------------------------------------
 // Device helpers
@@ -217,7 +226,7 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     return any;
 }
 
-constexpr int kHitCap = 8;   // hit-set capacity per lane (LDS); overflow -> exact list-walking DDA
+constexpr int kHitCap = PT_HITCAP;   // hit-set capacity per lane (LDS); overflow -> exact list-walking DDA
 
 // BLAS traversal collecting hit-set members: triangles the reference test
 // accepts, as (t bits, index, packed voxel box lo, hi) in the lane's LDS slots
@@ -568,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
 
 // One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
 template <bool FIRST, int ACCEL, int BS>
-__global__ __launch_bounds__(BS) void k_bounce(KParams p, int iter, int bounce) {
+__global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter, int bounce) {
     __shared__ int s_stack[(!FIRST && ACCEL != ACCEL_GRID) ? kStack * BS : 1];
     __shared__ int4 s_hs[(!FIRST && ACCEL == ACCEL_GRID_FAST) ? kHitCap * BS : 1];
     __shared__ int s_wave[BS / 64];

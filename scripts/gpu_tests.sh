@@ -3,5 +3,5 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
 rc=$?; tail -25 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python bench.py --steps 16 --warmup 2 > gpurun_out/bench_bvh.json 2> gpurun_out/bench_bvh.err
-rc=$?; cat gpurun_out/bench_bvh.json; tail -5 gpurun_out/bench_bvh.err; exit $rc
+timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; exit $rc
