@@ -34,6 +34,12 @@ constexpr int kBlock = 256;
 #ifndef PT_MINWAVES
 #define PT_MINWAVES 5
 #endif
+#ifndef PT_XCD_MAP
+#define PT_XCD_MAP 0      // 1: XCD-contiguous chunk mapping (measured 20% slower: off)
+#endif
+#ifndef PT_FMA_NODES
+#define PT_FMA_NODES 0    // 1: node slab tests as fma(lo, inv, -o*inv) (measured neutral: off)
+#endif
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
 
 // ---------------------------------------------------------------------------
@@ -152,11 +158,26 @@ __device__ bool grid_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3
     }
 }
 
-// Conservative slab test for BVH node boxes (boxes are padded at build time).
+// Inverse direction for node tests: clamped to +-1e30 so the FMA form never
+// meets inf * 0 or inf - inf (a zero direction component stays a huge slope).
+__device__ __forceinline__ f3 node_inv(f3 inv) {
+    return mk3(fminf(fmaxf(inv.x, -1e30f), 1e30f), fminf(fmaxf(inv.y, -1e30f), 1e30f), fminf(fmaxf(inv.z, -1e30f), 1e30f));
+}
+
+// Conservative slab test for BVH node boxes (boxes are padded at build time,
+// so the test need not follow the reference's rounding: the FMA form
+// lo * inv - o * inv is used, with o * inv hoisted per traversal).
 __device__ __forceinline__ void node_slab(const float* lo, const float* hi, f3 o, f3 inv, float& tn, float& tf) {
+#if PT_FMA_NODES
+    const f3 oi = o * inv;   // recomputed per call; the compiler hoists it out of the traversal loop
+    float a0 = __builtin_fmaf(lo[0], inv.x, -oi.x), b0 = __builtin_fmaf(hi[0], inv.x, -oi.x);
+    float a1 = __builtin_fmaf(lo[1], inv.y, -oi.y), b1 = __builtin_fmaf(hi[1], inv.y, -oi.y);
+    float a2 = __builtin_fmaf(lo[2], inv.z, -oi.z), b2 = __builtin_fmaf(hi[2], inv.z, -oi.z);
+#else
     float a0 = (lo[0] - o.x) * inv.x, b0 = (hi[0] - o.x) * inv.x;
     float a1 = (lo[1] - o.y) * inv.y, b1 = (hi[1] - o.y) * inv.y;
     float a2 = (lo[2] - o.z) * inv.z, b2 = (hi[2] - o.z) * inv.z;
+#endif
     tn = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fminf(a2, b2));
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
 }
@@ -423,10 +444,18 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     if (!slab_ref(M.bbox, o, d, inv, t_box)) return false;
     const f3 pt = o + d * t_box;
     if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) return false;
-    if (p.debug & 2) return bvh_closest<STRIDE>(p, M, o, d, inv, best, best_tri, stack);   // timing-only ablation
+    const f3 ninv = node_inv(inv);
+    if (p.debug & 2) return bvh_closest<STRIDE>(p, M, o, d, ninv, best, best_tri, stack);   // timing-only ablation
     float tmin;
-    int nh = bvh_collect<STRIDE, true>(p, M, o, d, inv, stack, hs, &tmin);
+    int nh = bvh_collect<STRIDE, true>(p, M, o, d, ninv, stack, hs, &tmin);
     if (nh == 0) return false;           // no accepted triangle anywhere on the ray: no hit voxel
+    if ((p.debug & 1) && nh > 0) {       // timing-only ablation: no walk
+        for (int h = 0; h < nh; h++) {
+            const float t = __int_as_float(hs[h * STRIDE].x);
+            if (t < best) { best = t; best_tri = hs[h * STRIDE].y; }
+        }
+        return true;
+    }
     WalkResult w;
     bool done = false;
     if (nh > 0) {
@@ -435,7 +464,7 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     }
     if (!done) {
         if (p.debug & 4) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);   // tier-2 counter (diagnostic)
-        nh = bvh_collect<STRIDE, false>(p, M, o, d, inv, stack, hs, &tmin);
+        nh = bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin);
         if (nh < 0) return grid_closest(p, M, o, d, inv, best, best_tri);   // overflow: exact slow path
         w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
     }
@@ -452,7 +481,7 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, in
     // triangle, or can only hit at a world distance > gdist (and `gdist > dd`
     // is strict).  Grid mode keeps the slab test's zero-direction quirk by
     // never miss-culling when a model-space direction component is 0.
-    const f3 winv = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    const f3 winv = node_inv(mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z));
     const float dlen = sqrtf(dot(dir, dir));
     for (int im = 0; im < p.nmodels; im++) {
         const ModelRec& M = p.models[im];
@@ -472,7 +501,7 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, in
         bool ok;
         if (ACCEL == ACCEL_GRID) ok = grid_closest(p, M, o, d, inv, best, best_tri);
         else if (ACCEL == ACCEL_GRID_FAST) ok = grid_hitset<STRIDE>(p, M, o, d, inv, best, best_tri, stack, hs);
-        else ok = bvh_closest<STRIDE>(p, M, o, d, inv, best, best_tri, stack);
+        else ok = bvh_closest<STRIDE>(p, M, o, d, node_inv(inv), best, best_tri, stack);
         if (ok) {
             const f3 nd = normalize(d);
             const f3 pm = o + nd * best;
@@ -582,7 +611,18 @@ __global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter,
     __shared__ int4 s_hs[(!FIRST && ACCEL == ACCEL_GRID_FAST) ? kHitCap * BS : 1];
     __shared__ int s_wave[BS / 64];
     const int n = FIRST ? p.npix : p.n_live[bounce];
-    const int j0 = blockIdx.x * BS;
+    // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md); map
+    // them so XCD x processes the contiguous chunk range [x q, (x+1) q) of the live
+    // pool -- neighbouring rays (neighbouring pixels' paths) share one L2.  The grid
+    // has nblocks + 8 workgroups so the permutation covers every live chunk.
+    int chunk = blockIdx.x;
+    if (PT_XCD_MAP) {
+        const int nact = (n + BS - 1) / BS;
+        const int q = (nact + 7) >> 3;
+        chunk = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
+        if ((int)(blockIdx.x >> 3) >= q) chunk = 0x7fffffff;
+    }
+    const int j0 = chunk >= (n + BS - 1) / BS ? n : chunk * BS;
     if (j0 >= n) return;                       // whole block idle (uniform)
     const int j = j0 + threadIdx.x;
     const bool active = j < n;
@@ -602,7 +642,7 @@ __global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter,
             h.model = p.cache_model[j];
         } else {
             // dense slot j -> (source block b, rank) via the scan of the previous bounce
-            int lo = p.dst_start[blockIdx.x], hi = p.dst_start[blockIdx.x + 1];
+            int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
@@ -650,23 +690,31 @@ __global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter,
         p.ray[out_buf][1][dst] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(r.bounces));
         p.ray[out_buf][2][dst] = make_float4(r.c.x, r.c.y, r.c.z, 0.0f);
     }
-    if (threadIdx.x == 0) p.blk_cnt[blockIdx.x] = total;
+    if (threadIdx.x == 0) p.blk_cnt[chunk] = total;
 }
 
 // One workgroup: exclusive scan of survivor counts of bounce `bounce`,
 // live count for bounce+1, and the first source block of every
 // destination block (dst_start).
 __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
+    // Counts are staged through LDS with coalesced loads (up to kScanLds chunks),
+    // each thread scans a contiguous run there, offsets go back coalesced.
+    constexpr int kScanLds = 32768;
+    __shared__ int s_v[kScanLds + 1];
     __shared__ int s_part[1024];
     __shared__ int s_total;
     const int tid = threadIdx.x;
     const int n = bounce == 0 ? p.npix : p.n_live[bounce];
     const int CH = p.chunk;
     const int nb = (n + CH - 1) / CH;
+    const bool staged = nb <= kScanLds;
+    if (staged)
+        for (int i = tid; i < nb; i += 1024) s_v[i] = p.blk_cnt[i];
+    __syncthreads();
     const int per = (nb + 1023) / 1024;
     const int s = tid * per, e = min(s + per, nb);
     int sum = 0;
-    for (int i = s; i < e; i++) sum += p.blk_cnt[i];
+    for (int i = s; i < e; i++) sum += staged ? s_v[i] : p.blk_cnt[i];
     s_part[tid] = sum;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
@@ -676,7 +724,11 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         __syncthreads();
     }
     int acc = s_part[tid] - sum;   // exclusive
-    for (int i = s; i < e; i++) { p.blk_off[i] = acc; acc += p.blk_cnt[i]; }
+    if (staged) {
+        for (int i = s; i < e; i++) { const int c = s_v[i]; s_v[i] = acc; acc += c; }
+    } else {
+        for (int i = s; i < e; i++) { const int c = p.blk_cnt[i]; p.blk_off[i] = acc; acc += c; }
+    }
     if (tid == 1023) {
         s_total = s_part[1023];
         p.blk_off[nb] = s_part[1023];
@@ -685,12 +737,17 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         if (bounce < kMaxBounceCounters) p.segments[1 + bounce] += (unsigned long long)n;
     }
     __syncthreads();
+    if (staged) {
+        s_v[nb] = s_total;
+        for (int i = tid; i < nb; i += 1024) p.blk_off[i] = s_v[i];
+        __syncthreads();
+    }
     const int total = s_total;
     for (int i = s; i < e; i++) {
-        const int c = p.blk_cnt[i];
-        if (c == 0) continue;
-        const int o0 = p.blk_off[i];
-        for (int bd = (o0 + CH - 1) / CH; bd * CH < o0 + c; bd++) p.dst_start[bd] = i;
+        const int o0 = staged ? s_v[i] : p.blk_off[i];                  // this thread's own writes
+        const int o1 = staged ? s_v[i + 1] : o0 + p.blk_cnt[i];
+        if (o1 == o0) continue;
+        for (int bd = (o0 + CH - 1) / CH; bd * CH < o1; bd++) p.dst_start[bd] = i;
     }
     if (tid == 0) p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
 }
@@ -886,7 +943,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             hipEventDestroy(e0); hipEventDestroy(e1);
         }
     }
-    const dim3 grid((unsigned)kp.nblocks);
+    const dim3 grid((unsigned)kp.nblocks + 8u);
     const int passes = cfg.max_bounces > 1 ? cfg.max_bounces : 1;
     for (int it = 0; it < n_iters; it++) {
         const int iter = first_iter + it;
