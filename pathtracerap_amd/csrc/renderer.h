@@ -56,6 +56,9 @@ struct KParams {
     int* n_live;                // live rays per bounce
     unsigned long long* segments;      // [0] total, [1 + b] live rays entering bounce b, [65] diagnostics
     int debug;                          // timing-only ablation switches (PT_DEBUG_ABLATE); 0 in production
+    int4* hs_pool;                      // ACCEL_GRID_FAST overflow hit sets (64-member blocks)
+    int* hs_pool_next;                  // bump allocator, reset by k_scan every bounce
+    int hs_pool_blocks;
 };
 
 constexpr int kMaxBounceCounters = 64;

@@ -247,14 +247,15 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     return any;
 }
 
-constexpr int kHitCap = PT_HITCAP;   // hit-set capacity per lane (LDS); overflow -> exact list-walking DDA
+constexpr int kHitCap = PT_HITCAP;   // hit-set capacity per lane (LDS); overflow -> global pool block
+constexpr int kHitCapPool = 64;      // global pool block (members); overflow -> exact list-walking DDA
 
 // BLAS traversal collecting hit-set members: triangles the reference test
 // accepts, as (t bits, index, packed voxel box lo, hi) in the lane's LDS slots
 // hs[i * STRIDE].  BOUNDED: only members with t <= t_min + 2R are required
 // (nodes entered beyond that are pruned; extra members are harmless).
 // Returns the count (-1 on overflow); *tmin_out = smallest t accepted.
-template <int STRIDE, bool BOUNDED>
+template <int STRIDE, bool BOUNDED, int HSTRIDE = STRIDE, int CAP = kHitCap>
 __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, int* __restrict__ stack,
                            int4* __restrict__ hs, float* tmin_out) {
     int nh = 0;
@@ -291,20 +292,20 @@ __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 i
                     if (BOUNDED) {
                         if (t < tmin) tmin = t;
                         if (t > tmin + margin) continue;          // not required (NaN is kept)
-                        if (nh == kHitCap) {                       // drop members now beyond the bound
+                        if (nh == CAP) {                           // drop members now beyond the bound
                             int w = 0;
                             for (int q = 0; q < nh; q++) {
-                                const int4 e = hs[q * STRIDE];
-                                if (!(__int_as_float(e.x) > tmin + margin)) hs[(w++) * STRIDE] = e;
+                                const int4 e = hs[q * HSTRIDE];
+                                if (!(__int_as_float(e.x) > tmin + margin)) hs[(w++) * HSTRIDE] = e;
                             }
                             nh = w;
                         }
                     } else if (t < tmin) {
                         tmin = t;
                     }
-                    if (nh == kHitCap) return -1;
-                    hs[nh * STRIDE] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
-                                                __float_as_int(C.w));
+                    if (nh == CAP) return -1;
+                    hs[nh * HSTRIDE] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
+                                                 __float_as_int(C.w));
                     nh++;
                 }
             }
@@ -350,7 +351,7 @@ struct WalkResult {
 // depend on V, so V is a hit voxel iff some member's box contains V.  The
 // reference keeps the first strict minimum in test order (voxel order, then
 // ascending index inside a list): the lexicographic minimum of (t, step, index).
-template <int STRIDE>
+template <int HSTRIDE>
 __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                   const int4* __restrict__ hs, int nh, float tmin) {
     const int GX = p.gdim[0], GY = p.gdim[1], GZ = p.gdim[2];
@@ -373,25 +374,25 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
     // union of the members' voxel boxes: outside it no voxel is a hit voxel
     int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
     for (int h = 0; h < nh; h++) {
-        const int4 e = hs[h * STRIDE];
+        const int4 e = hs[h * HSTRIDE];
         ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
         uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
     }
-    const unsigned all = (1u << nh) - 1u;
+    const unsigned long long all = nh >= 64 ? ~0ull : ((1ull << nh) - 1ull);
     int cx = 0, cy = 0, cz = 0;
     bool hit = false;
-    unsigned tested = 0;
+    unsigned long long tested = 0;
     float bt = kFMax;
     int bk = -1, bi = -1;
     for (int k = 0;; k++) {
         bool vhit = false;
         if (ix >= ulx && ix <= uhx && iy >= uly && iy <= uhy && iz >= ulz && iz <= uhz) {
             for (int h = 0; h < nh; h++) {
-                const int4 e = hs[h * STRIDE];
+                const int4 e = hs[h * HSTRIDE];
                 if (vbox_has(e.z, e.w, ix, iy, iz)) {
                     vhit = true;
-                    if (!((tested >> h) & 1u)) {
-                        tested |= 1u << h;
+                    if (!((tested >> h) & 1ull)) {
+                        tested |= 1ull << h;
                         const float t = __int_as_float(e.x);
                         if (t < bt || (t == bt && (k < bk || (k == bk && e.y < bi)))) { bt = t; bk = k; bi = e.y; }
                     }
@@ -429,6 +430,27 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
     return w;
 }
 
+// Overflow tiers of grid_hitset: bounded, then unbounded collection into a
+// kHitCapPool-member block bump-allocated from the global pool (k_scan resets
+// the pool every bounce).  Returns false when the pool is exhausted or the
+// block overflows too (the caller then runs the list-walking DDA).
+template <int STRIDE>
+__device__ bool grid_hitset_pool(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, f3 ninv,
+                                              f3 pt, float t_box, int* __restrict__ stack, WalkResult& w) {
+    const int blk = atomicAdd(p.hs_pool_next, 1);
+    if (blk >= p.hs_pool_blocks) return false;
+    int4* g = p.hs_pool + (size_t)blk * kHitCapPool;
+    float tmin;
+    int ng = bvh_collect<STRIDE, true, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin);
+    if (ng < 0) return false;
+    w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin);
+    if (w.final_min || w.tw < tmin + M.reach) return true;
+    ng = bvh_collect<STRIDE, false, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin);
+    if (ng < 0) return false;
+    w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin);
+    return true;
+}
+
 // computeRayGridIntersection (Renderer.cpp:238-360), result-identical, via the
 // BLAS hit set and hitset_walk.
 // Tier 1 collects members with t <= t_min + 2R only (R = ModelRec::reach: a
@@ -461,12 +483,24 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     if (nh > 0) {
         w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
         done = w.final_min || w.tw < tmin + M.reach;
+        if (!done) {                                                       // tier 2 in LDS
+            if (p.debug & 4) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);
+            nh = bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin);
+            if (nh >= 0) {
+                w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
+                done = true;
+            }
+        }
     }
     if (!done) {
-        if (p.debug & 4) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);   // tier-2 counter (diagnostic)
-        nh = bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin);
-        if (nh < 0) return grid_closest(p, M, o, d, inv, best, best_tri);   // overflow: exact slow path
-        w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
+        // LDS hit set overflowed: the same two tiers in a 64-entry block of the
+        // global pool (cold path, kept out of line).
+        if (p.debug & 4) atomicAdd(p.segments + 2 + kMaxBounceCounters, 1ull);
+        done = grid_hitset_pool<STRIDE>(p, M, o, d, inv, ninv, pt, t_box, stack, w);
+        if (!done) {
+            if (p.debug & 4) atomicAdd(p.segments + 3 + kMaxBounceCounters, 1ull);
+            return grid_closest(p, M, o, d, inv, best, best_tri);   // exact list-walking DDA
+        }
     }
     if (w.hit && w.has_best) { best = w.t; best_tri = w.tri; }
     return w.hit;
@@ -749,7 +783,10 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         if (o1 == o0) continue;
         for (int bd = (o0 + CH - 1) / CH; bd * CH < o1; bd++) p.dst_start[bd] = i;
     }
-    if (tid == 0) p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
+    if (tid == 0) {
+        p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
+        *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
+    }
 }
 
 __global__ void k_selftest_math(int n, const float* x, const float* y, float* out) {
@@ -873,8 +910,12 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.blk_off, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.dst_start, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.n_live, nullptr, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.segments, nullptr, (2 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, (2 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    kp.hs_pool_blocks = cfg.accel == ACCEL_GRID_FAST ? 65536 : 1;     // 64 MiB of 64-member blocks
+    PT_HIP(upload(allocs, &kp.hs_pool, nullptr, (size_t)kp.hs_pool_blocks * kHitCapPool * sizeof(int4), stream));
+    PT_HIP(upload(allocs, &kp.hs_pool_next, nullptr, sizeof(int), stream));
+    PT_HIP(hipMemsetAsync(kp.hs_pool_next, 0, sizeof(int), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (4 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (4 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -891,6 +932,7 @@ int Renderer::clearImage() {
 }
 
 int Renderer::launchPrimary() {
+    PT_HIP(hipMemsetAsync(kp.hs_pool_next, 0, sizeof(int), stream));
     const dim3 grid((unsigned)((kp.npix + kBlock - 1) / kBlock));
     if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL(k_primary<ACCEL_BVH>, grid, dim3(kBlock), 0, stream, kp);
     else if (cfg.accel == ACCEL_GRID_FAST) hipLaunchKernelGGL(k_primary<ACCEL_GRID_FAST>, grid, dim3(kBlock), 0, stream, kp);
@@ -1018,11 +1060,11 @@ long long Renderer::segments() {
 
 int Renderer::segmentsPerBounce(long long* out, int n) {
     if (!allocated) { last_error = "not allocated"; return -1; }
-    unsigned long long v[2 + kMaxBounceCounters];
+    unsigned long long v[4 + kMaxBounceCounters];
     PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n && i < kMaxBounceCounters + 1; i++) out[i] = (long long)v[1 + i];
-    for (int i = kMaxBounceCounters + 1; i < n; i++) out[i] = 0;
+    for (int i = 0; i < n && i < kMaxBounceCounters + 3; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters + 3; i < n; i++) out[i] = 0;
     return 0;
 }
 
@@ -1088,6 +1130,7 @@ int Renderer::intersectRays(int n, const float* orig, const float* dir, float* d
     PT_HIP(hipMalloc(&d_m, n * 4));
     PT_HIP(hipMemcpyAsync(d_o, orig, n * 12, hipMemcpyHostToDevice, stream));
     PT_HIP(hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, stream));
+    PT_HIP(hipMemsetAsync(kp.hs_pool_next, 0, sizeof(int), stream));
     const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
     if (cfg.accel == ACCEL_BVH) hipLaunchKernelGGL(k_intersect_rays<ACCEL_BVH>, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_t, d_n, d_m);
     else if (cfg.accel == ACCEL_GRID_FAST)

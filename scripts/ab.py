@@ -60,9 +60,9 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
-        diag = rs[v].segments_per_bounce(65)[64]
-        if diag:
-            out[v]["diag_counter"] = diag
+        diag = rs[v].segments_per_bounce(67)[64:67]
+        if any(diag):
+            out[v]["diag_tier2_t1overflow_fallback"] = diag
     print(json.dumps(out, indent=1))
 
 
