@@ -94,6 +94,21 @@ def cpu_baseline(scene_path, accel_name, bounces, width, height, target_s):
                       f"{seg} segments in {dt:.2f}s on {threads} thread(s)"}
 
 
+def workload_name(args):
+    """Label of the BASELINE.json configuration this run measures."""
+    default = (args.ntri == 100_000 and args.width == 1280 and args.height == 1024 and args.bounces == 8
+               and not args.metallic)
+    if default:
+        return "configs[1]: diffuse-only synthetic OBJ (~100k tris), 1280x1024, 8 bounces"
+    kind = "metallic+diffuse" if args.metallic else "diffuse-only"
+    tag = {(True, 2800): "configs[2] shape: ", (False, 1280): ""}.get((args.metallic, args.width), "")
+    if not args.metallic and args.ntri >= 5_000_000:
+        tag = "configs[4] shape: "
+    elif not args.metallic and args.ntri >= 500_000:
+        tag = "north_star target shape: "
+    return f"{tag}{kind} synthetic OBJ (~{args.ntri} tris), {args.width}x{args.height}, {args.bounces} bounces"
+
+
 def load_pmc(kernel, workload_key):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC
     summary (scripts/pmc_summary.py), corrected per MI355X_MICROARCH.md
@@ -253,7 +268,7 @@ def main():
             "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "samples_per_sec": round(samples, 1),
-            "config": {"workload": "configs[1]: diffuse-only synthetic OBJ (~100k tris), 1280x1024, 8 bounces"
+            "config": {"workload": workload_name(args)
                                    + (" [metallic variant]" if args.metallic else ""),
                        "triangles": ntri, "width": cfg.width, "height": cfg.height, "bounces": cfg.max_bounces,
                        "spp_per_step": 1, "accel": args.accel,
