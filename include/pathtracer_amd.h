@@ -118,6 +118,9 @@ int pt_renderer_set_profiling(pt_renderer *r, int on);
 /* stats[0..6] = secondary-bounce ms, scan ms, primary ms, secondary-bounce launches,
  * scan launches, first-bounce ms, first-bounce launches (HIP events; resets). */
 int pt_renderer_kernel_stats(pt_renderer *r, double stats[7]);
+/* Same, n values: stats[7..8] = persistent-trace ms, launches (ACCEL_BVH splits each
+ * secondary bounce into k_trace_bvh + a shading pass; stats[0] is then the shading pass). */
+int pt_renderer_kernel_stats_ex(pt_renderer *r, double *stats, int n);
 /* Test hooks: primary-hit cache and batch intersection (host arrays). */
 int pt_renderer_primary_hits(pt_renderer *r, float *dist, float *normal, int *model);
 int pt_renderer_intersect_rays(pt_renderer *r, int n, const float *orig, const float *dir,

@@ -94,6 +94,7 @@ EXPORTS = [
     ("pt_renderer_segments_per_bounce", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("pt_renderer_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("pt_renderer_kernel_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    ("pt_renderer_kernel_stats_ex", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("pt_renderer_primary_hits", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_F, _P_I]),
     ("pt_renderer_intersect_rays", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _P_F, _P_F, _P_F, _P_F, _P_I]),
     ("pt_renderer_free", None, [ctypes.c_void_p]),
@@ -310,11 +311,12 @@ class Renderer:
         _err(lib().pt_renderer_set_profiling(self._h, 1 if on else 0), "set_profiling")
 
     def kernel_stats(self) -> dict:
-        st = (ctypes.c_double * 7)()
-        _err(lib().pt_renderer_kernel_stats(self._h, st), "kernel_stats")
+        st = (ctypes.c_double * 9)()
+        _err(lib().pt_renderer_kernel_stats_ex(self._h, st, 9), "kernel_stats")
         return dict(bounce_ms=st[0], scan_ms=st[1], primary_ms=st[2],
                     bounce_launches=int(st[3]), scan_launches=int(st[4]),
-                    first_ms=st[5], first_launches=int(st[6]))
+                    first_ms=st[5], first_launches=int(st[6]),
+                    trace_ms=st[7], trace_launches=int(st[8]))
 
     def primary_hits(self):
         n = self.cfg.width * self.cfg.height

@@ -9,6 +9,7 @@
 // cap) so the kernels' fixed LDS traversal stack cannot overflow.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -18,7 +19,15 @@ namespace pt {
 
 namespace {
 
-constexpr int kLeafMax = 4;
+// Leaf size; PT_BVH_LEAF overrides it for build experiments (1..16).
+int leaf_max() {
+    static const int v = [] {
+        const char* e = std::getenv("PT_BVH_LEAF");
+        const int x = e ? std::atoi(e) : 2;
+        return x >= 1 && x <= 16 ? x : 2;
+    }();
+    return v;
+}
 constexpr int kBins = 16;
 constexpr int kMaxDepth = 23;   // <= the kernels' LDS stack (PT_STACK = 24 entries)
 
@@ -64,6 +73,7 @@ struct Builder {
         Box box, cbox;
         for (int i = b; i < e; i++) { box.grow(refs[i].box); cbox.grow(refs[i].c); }
         const int n = e - b;
+        const int kLeafMax = leaf_max();
         if (n <= kLeafMax || depth >= kMaxDepth) return leaf(b, e, box);   // depth cap: a (rare) larger leaf
         // Force balanced splits when the remaining depth budget is tight.
         const bool force_median = depth + ceil_log2((n + kLeafMax - 1) / kLeafMax) >= kMaxDepth - 1;

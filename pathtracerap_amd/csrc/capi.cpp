@@ -217,6 +217,15 @@ int pt_renderer_kernel_stats(pt_renderer* r, double st[7]) {
     st[5] = k.first_ms; st[6] = (double)k.first_launches;
     return 0;
 }
+int pt_renderer_kernel_stats_ex(pt_renderer* r, double* st, int n) {
+    if (!r || !r->r || !st || n < 0) return set_err("bad arguments");
+    pt::KernelStats k;
+    if (r->r->kernelStats(&k) < 0) return set_err(r->r->last_error);
+    const double v[9] = {k.bounce_ms, k.scan_ms, k.primary_ms, (double)k.bounce_launches, (double)k.scan_launches,
+                         k.first_ms, (double)k.first_launches, k.trace_ms, (double)k.trace_launches};
+    for (int i = 0; i < n; i++) st[i] = i < 9 ? v[i] : 0.0;
+    return 0;
+}
 int pt_renderer_primary_hits(pt_renderer* r, float* d, float* n, int* m) {
     if (!d || !n || !m) return set_err("null buffer");
     R_CALL(r->r->primaryHits(d, n, m));

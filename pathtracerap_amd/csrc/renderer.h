@@ -59,13 +59,18 @@ struct KParams {
     int4* hs_pool;                      // ACCEL_GRID_FAST overflow hit sets (64-member blocks)
     int* hs_pool_next;                  // bump allocator, reset by k_scan every bounce
     int hs_pool_blocks;
+    float4* hit4;                       // split trace/shade (ACCEL_BVH): per-slot dist, normal
+    int* hitm;                          // per-slot model
+    int* trace_next;                    // persistent trace work counter, reset by k_scan
+    int trace_refill;                   // refill a wave's idle lanes once this many are idle
 };
 
 constexpr int kMaxBounceCounters = 64;
 
 struct KernelStats {
-    double bounce_ms = 0, scan_ms = 0, primary_ms = 0, first_ms = 0;
+    double bounce_ms = 0, scan_ms = 0, primary_ms = 0, first_ms = 0, trace_ms = 0;
     long long bounce_launches = 0, scan_launches = 0, first_launches = 0;   // bounce_* = secondary bounces
+    long long trace_launches = 0;        // k_trace_bvh (split trace/shade); bounce_* is then the shading pass
 };
 
 class Renderer {
@@ -94,7 +99,7 @@ public:
 
 private:
     int launchPrimary();
-    void launchBounce(bool first, dim3 grid, int iter, int b);
+    void launchBounce(bool first, dim3 grid, int iter, int b, int accel);
     int fail(hipError_t e, const char* what);
     void freeBuffers();
 
@@ -108,7 +113,9 @@ private:
     float* ext_image = nullptr;
     bool profiling = false;
     std::vector<void*> allocs;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events, trace_events;
+    bool split_trace = false;        // ACCEL_BVH: persistent k_trace_bvh + shading pass
+    int trace_blocks = 0;
     KernelStats stats;
 };
 

@@ -40,6 +40,7 @@ constexpr int kBlock = 256;
 #ifndef PT_FMA_NODES
 #define PT_FMA_NODES 0    // 1: node slab tests as fma(lo, inv, -o*inv) (measured neutral: off)
 #endif
+constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
 
 // ---------------------------------------------------------------------------
@@ -182,6 +183,65 @@ __device__ __forceinline__ void node_slab(const float* lo, const float* hi, f3 o
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
 }
 
+// One node visit of the closest-hit BLAS traversal: test both child boxes,
+// run the triangle tests of hit leaf children, then descend (pushing the far
+// child) or pop.  Returns true when the traversal has finished.  Shared by the
+// per-ray loop (bvh_closest) and the persistent trace kernel (k_trace_bvh).
+template <int STRIDE>
+__device__ __forceinline__ bool bvh_step(const KParams& p, f3 o, f3 d, f3 inv, int& cur, int& sp,
+                                         int* __restrict__ stack, float& best, int& best_tri, bool& any,
+                                         int& n_tris) {
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+    const float4 q0 = nodes[4 * cur + 0];
+    const float4 q1 = nodes[4 * cur + 1];
+    const float4 q2 = nodes[4 * cur + 2];
+    const float4 q3 = nodes[4 * cur + 3];
+    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+    const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+    const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+    const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+    float tn0, tf0, tn1, tf1;
+    node_slab(lo0, hi0, o, inv, tn0, tf0);
+    node_slab(lo1, hi1, o, inv, tn1, tf1);
+    bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
+    bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const bool hc = c == 0 ? h0 : h1;
+        const int cc = c == 0 ? cnt0 : cnt1;
+        const int lc = c == 0 ? link0 : link1;
+        if (hc && cc > 0) {
+            for (int i = lc; i < lc + cc; i++) {
+                const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
+                const int it = __float_as_int(A.w);
+                float t;
+                n_tris++;
+                if (tri_test_rec(A, B, C, o, d, t)) {
+                    any = true;
+                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+                }
+            }
+        }
+    }
+    h0 = h0 && cnt0 == 0;
+    h1 = h1 && cnt1 == 0;
+    if (h0 && h1) {
+        const bool first0 = tn0 <= tn1;
+        stack[sp * STRIDE] = first0 ? link1 : link0;
+        sp++;
+        cur = first0 ? link0 : link1;
+    } else if (h0) {
+        cur = link0;
+    } else if (h1) {
+        cur = link1;
+    } else {
+        if (sp == 0) return true;
+        sp--;
+        cur = stack[sp * STRIDE];
+    }
+    return false;
+}
+
 // Exact closest hit over the mesh's triangles via its BLAS.  Matches the
 // brute-force scan in triangle-index order: (t, index) lexicographic minimum.
 template <int STRIDE>
@@ -190,59 +250,15 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     bool any = false;
     int sp = 0;
     int cur = M.bvh_root;
-    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+    int n_nodes = 0, n_tris = 0;     // PT_DEBUG_ABLATE & 8 statistics
     for (;;) {
-        const float4 q0 = nodes[4 * cur + 0];
-        const float4 q1 = nodes[4 * cur + 1];
-        const float4 q2 = nodes[4 * cur + 2];
-        const float4 q3 = nodes[4 * cur + 3];
-        const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-        const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-        const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-        const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-        float tn0, tf0, tn1, tf1;
-        node_slab(lo0, hi0, o, inv, tn0, tf0);
-        node_slab(lo1, hi1, o, inv, tn1, tf1);
-        bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
-        bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
-        if (h0 && cnt0 > 0) {
-            for (int i = link0; i < link0 + cnt0; i++) {
-                const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
-                const int it = __float_as_int(A.w);
-                float t;
-                if (tri_test_rec(A, B, C, o, d, t)) {
-                    any = true;
-                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
-                }
-            }
-            h0 = false;
-        }
-        if (h1 && cnt1 > 0) {
-            for (int i = link1; i < link1 + cnt1; i++) {
-                const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
-                const int it = __float_as_int(A.w);
-                float t;
-                if (tri_test_rec(A, B, C, o, d, t)) {
-                    any = true;
-                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
-                }
-            }
-            h1 = false;
-        }
-        if (h0 && h1) {
-            const bool first0 = tn0 <= tn1;
-            stack[sp * STRIDE] = first0 ? link1 : link0;
-            sp++;
-            cur = first0 ? link0 : link1;
-        } else if (h0) {
-            cur = link0;
-        } else if (h1) {
-            cur = link1;
-        } else {
-            if (sp == 0) break;
-            sp--;
-            cur = stack[sp * STRIDE];
-        }
+        n_nodes++;
+        if (bvh_step<STRIDE>(p, o, d, inv, cur, sp, stack, best, best_tri, any, n_tris)) break;
+    }
+    if (p.debug & 8) {
+        atomicAdd(p.segments + 4 + kMaxBounceCounters, (unsigned long long)n_nodes);
+        atomicAdd(p.segments + 5 + kMaxBounceCounters, (unsigned long long)n_tris);
+        atomicAdd(p.segments + 6 + kMaxBounceCounters, 1ull);
     }
     return any;
 }
@@ -506,44 +522,33 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     return w.hit;
 }
 
-template <int ACCEL, int STRIDE>
-__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs) {
-    float gdist = kFMax;
-    int gmodel = -1, gtri = -1;
-    // Instance culling against each model's conservative world box.  Exact:
-    // a culled instance either cannot pass the reference's slab test / hit a
-    // triangle, or can only hit at a world distance > gdist (and `gdist > dd`
-    // is strict).  Grid mode keeps the slab test's zero-direction quirk by
-    // never miss-culling when a model-space direction component is 0.
-    const f3 winv = node_inv(mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z));
-    const float dlen = sqrtf(dot(dir, dir));
-    for (int im = 0; im < p.nmodels; im++) {
-        const ModelRec& M = p.models[im];
-        float wtn, wtf;
-        node_slab(M.wbox, M.wbox + 3, orig, winv, wtn, wtf);
-        if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;          // cannot beat the current hit
-        if (wtn > wtf || wtf * dlen < -1.0f) {                        // misses the instance box
-            if (ACCEL == ACCEL_BVH) continue;
-            const f3 dm = xform12(M.w2m, dir, 0.0f);
-            if (dm.x != 0.0f && dm.y != 0.0f && dm.z != 0.0f) continue;
-        }
-        const f3 o = xform12(M.w2m, orig, 1.0f);
-        const f3 d = normalize(xform12(M.w2m, dir, 0.0f));
-        const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
-        float best = kFMax;
-        int best_tri = -1;
-        bool ok;
-        if (ACCEL == ACCEL_GRID) ok = grid_closest(p, M, o, d, inv, best, best_tri);
-        else if (ACCEL == ACCEL_GRID_FAST) ok = grid_hitset<STRIDE>(p, M, o, d, inv, best, best_tri, stack, hs);
-        else ok = bvh_closest<STRIDE>(p, M, o, d, node_inv(inv), best, best_tri, stack);
-        if (ok) {
-            const f3 nd = normalize(d);
-            const f3 pm = o + nd * best;
-            const f3 pw = xform12(M.m2w, pm, 1.0f);
-            const float dd = length(pw - orig);
-            if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
-        }
+// Instance culling against a model's conservative world box.  Exact: a
+// culled instance either cannot pass the reference's slab test / hit a
+// triangle, or can only hit at a world distance > gdist (and `gdist > dd`
+// is strict).  Grid mode keeps the slab test's zero-direction quirk by never
+// miss-culling when a model-space direction component is 0.
+template <int ACCEL>
+__device__ __forceinline__ bool model_culled(const ModelRec& M, f3 orig, f3 dir, f3 winv, float dlen, float gdist) {
+    float wtn, wtf;
+    node_slab(M.wbox, M.wbox + 3, orig, winv, wtn, wtf);
+    if (wtn * dlen > gdist * 1.0001f + 0.01f) return true;           // cannot beat the current hit
+    if (wtn > wtf || wtf * dlen < -1.0f) {                            // misses the instance box
+        if (ACCEL == ACCEL_BVH) return true;
+        const f3 dm = xform12(M.w2m, dir, 0.0f);
+        if (dm.x != 0.0f && dm.y != 0.0f && dm.z != 0.0f) return true;
     }
+    return false;
+}
+
+// World distance of a model-space hit (computeRaySceneIntersectionKernel, Renderer.cpp:386-397).
+__device__ __forceinline__ float model_hit_dist(const ModelRec& M, f3 o, f3 d, float best, f3 orig) {
+    const f3 nd = normalize(d);
+    const f3 pm = o + nd * best;
+    const f3 pw = xform12(M.m2w, pm, 1.0f);
+    return length(pw - orig);
+}
+
+__device__ __forceinline__ Hit make_hit(const KParams& p, float gdist, int gmodel, int gtri) {
     Hit h;
     h.dist = kFMax;
     h.n = mk3(0, 0, 0);
@@ -555,6 +560,32 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, in
         h.n = normalize(xform_normal9(p.models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
     }
     return h;
+}
+
+template <int ACCEL, int STRIDE>
+__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs) {
+    float gdist = kFMax;
+    int gmodel = -1, gtri = -1;
+    const f3 winv = node_inv(mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z));
+    const float dlen = sqrtf(dot(dir, dir));
+    for (int im = 0; im < p.nmodels; im++) {
+        const ModelRec& M = p.models[im];
+        if (model_culled<ACCEL>(M, orig, dir, winv, dlen, gdist)) continue;
+        const f3 o = xform12(M.w2m, orig, 1.0f);
+        const f3 d = normalize(xform12(M.w2m, dir, 0.0f));
+        const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+        float best = kFMax;
+        int best_tri = -1;
+        bool ok;
+        if (ACCEL == ACCEL_GRID) ok = grid_closest(p, M, o, d, inv, best, best_tri);
+        else if (ACCEL == ACCEL_GRID_FAST) ok = grid_hitset<STRIDE>(p, M, o, d, inv, best, best_tri, stack, hs);
+        else ok = bvh_closest<STRIDE>(p, M, o, d, node_inv(inv), best, best_tri, stack);
+        if (ok) {
+            const float dd = model_hit_dist(M, o, d, best, orig);
+            if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
+        }
+    }
+    return make_hit(p, gdist, gmodel, gtri);
 }
 
 // generateRaysKernel (Renderer.cpp:521-555)
@@ -638,10 +669,117 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
     model[i] = h.model;
 }
 
+// Dense slot j of bounce `bounce` -> its index in the ray pool written by the
+// previous bounce (block-local compaction + k_scan offsets).
+__device__ __forceinline__ int slot_source(const KParams& p, int j) {
+    const int chunk = j / p.chunk;
+    int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    return lo * p.chunk + (j - p.blk_off[lo]);
+}
+
+// Persistent BLAS trace for one bounce (ACCEL_BVH): computeRaySceneIntersectionKernel
+// (Renderer.cpp:363-409) for every live slot, result-identical to
+// intersect_scene<ACCEL_BVH>, written to the hit buffer the shading pass reads.
+// Each lane runs its own ray through (model select -> node visits) one step
+// per loop iteration and fetches a new slot from a global counter when its
+// ray is done, so a wave's lanes stay busy instead of idling behind the
+// wave's longest ray (secondary rays are incoherent).  Every wave exits once
+// the counter passes n and its lanes are idle.
+template <int BS>
+__global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
+    __shared__ int s_stack[kStack * BS];
+    int* stack = s_stack + threadIdx.x;
+    const int n = p.n_live[bounce];
+    const int in_buf = (bounce + 1) & 1;
+    const int lane = threadIdx.x & 63;
+    // lane state: 0 = needs a ray, 1 = select next model, 2 = traversing, 3 = no more rays
+    int state = 0;
+    int j = -1;
+    f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
+    float dlen = 0.0f, gdist = kFMax;
+    int gmodel = -1, gtri = -1, im = -1;
+    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0);
+    int cur = 0, sp = 0, best_tri = -1, n_tris = 0;
+    float best = kFMax;
+    bool any = false, exhausted = false;
+    for (unsigned iters = 0;; iters++) {
+        // refill idle lanes (wave-aggregated atomic) once enough are idle
+        const unsigned long long idle = __ballot(state == 0);
+        const unsigned long long busy = __ballot(state == 1 || state == 2);
+        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+            const int cnt = __popcll(idle);
+            const int leader = __ffsll((long long)idle) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.trace_next, cnt);
+            base = __shfl(base, leader);
+            if (base + cnt >= n) exhausted = true;
+            if (state == 0) {
+                j = base + __popcll(idle & ((1ull << lane) - 1ull));
+                if (j < n) {
+                    const int src = slot_source(p, j);
+                    const float4 a = p.ray[in_buf][0][src];
+                    const float4 b = p.ray[in_buf][1][src];
+                    ow = mk3(a.x, a.y, a.z);
+                    dw = mk3(b.x, b.y, b.z);
+                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                    dlen = sqrtf(dot(dw, dw));
+                    gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
+                    state = 1;
+                } else {
+                    state = 3;
+                }
+            }
+        }
+        if (exhausted && state == 0) state = 3;
+        if (__ballot(state != 3) == 0) break;
+        if (iters > (1u << 26)) {                       // safety net: never spin forever
+            if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
+            break;
+        }
+        if (state == 1) {                               // advance to the next model that survives culling
+            for (;;) {
+                im++;
+                if (im >= p.nmodels) {
+                    const Hit h = make_hit(p, gdist, gmodel, gtri);
+                    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+                    p.hitm[j] = h.model;
+                    state = 0;
+                    break;
+                }
+                const ModelRec& M = p.models[im];
+                if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                o = xform12(M.w2m, ow, 1.0f);
+                d = normalize(xform12(M.w2m, dw, 0.0f));
+                ninv = node_inv(mk3(1 / d.x, 1 / d.y, 1 / d.z));
+                cur = M.bvh_root;
+                sp = 0;
+                best = kFMax;
+                best_tri = -1;
+                any = false;
+                state = 2;
+                break;
+            }
+        }
+        if (state == 2) {
+            if (bvh_step<BS>(p, o, d, ninv, cur, sp, stack, best, best_tri, any, n_tris)) {
+                if (any) {
+                    const float dd = model_hit_dist(p.models[im], o, d, best, ow);
+                    if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
+                }
+                state = 1;
+            }
+        }
+    }
+}
+
 // One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
 template <bool FIRST, int ACCEL, int BS>
 __global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter, int bounce) {
-    __shared__ int s_stack[(!FIRST && ACCEL != ACCEL_GRID) ? kStack * BS : 1];
+    __shared__ int s_stack[(!FIRST && ACCEL != ACCEL_GRID && ACCEL != kAccelHitBuffer) ? kStack * BS : 1];
     __shared__ int4 s_hs[(!FIRST && ACCEL == ACCEL_GRID_FAST) ? kHitCap * BS : 1];
     __shared__ int s_wave[BS / 64];
     const int n = FIRST ? p.npix : p.n_live[bounce];
@@ -688,7 +826,14 @@ __global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter,
             r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
             r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
             r.c = mk3(c.x, c.y, c.z);
-            h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
+            if (ACCEL == kAccelHitBuffer) {       // traced by k_trace_bvh
+                const float4 hh = p.hit4[j];
+                h.dist = hh.x;
+                h.n = mk3(hh.y, hh.z, hh.w);
+                h.model = p.hitm[j];
+            } else {
+                h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
+            }
         }
         shade(p, r, h, iter, j);
     }
@@ -786,6 +931,7 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
     if (tid == 0) {
         p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
+        *p.trace_next = 0;         // and an unclaimed persistent-trace counter
     }
 }
 
@@ -914,8 +1060,25 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.hs_pool, nullptr, (size_t)kp.hs_pool_blocks * kHitCapPool * sizeof(int4), stream));
     PT_HIP(upload(allocs, &kp.hs_pool_next, nullptr, sizeof(int), stream));
     PT_HIP(hipMemsetAsync(kp.hs_pool_next, 0, sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.segments, nullptr, (4 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, (4 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    {
+        // Persistent trace (ACCEL_BVH): hit buffer + work counter; PT_TRACE_SPLIT=0 keeps the fused kernel.
+        const char* e = std::getenv("PT_TRACE_SPLIT");
+        split_trace = cfg.accel == ACCEL_BVH && !(e && std::atoi(e) == 0);
+        const char* rf = std::getenv("PT_TRACE_REFILL");
+        kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
+        const int w = wpc ? std::max(1, std::atoi(wpc)) : 20;
+        trace_blocks = std::max(1, cus) * w;
+        const size_t hcap = split_trace ? cap : 1;
+        PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
+        PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
+        PT_HIP(upload(allocs, &kp.trace_next, nullptr, sizeof(int), stream));
+        PT_HIP(hipMemsetAsync(kp.trace_next, 0, sizeof(int), stream));
+    }
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (8 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (8 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -944,25 +1107,27 @@ int Renderer::launchPrimary() {
 
 template <bool FIRST, int BS>
 static void launch_bounce_bs(int accel, dim3 grid, hipStream_t st, const KParams& kp, int iter, int b) {
-    if (accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_BVH, BS>), grid, dim3(BS), 0, st, kp, iter, b);
+    if (accel == kAccelHitBuffer)
+        hipLaunchKernelGGL((k_bounce<FIRST, kAccelHitBuffer, BS>), grid, dim3(BS), 0, st, kp, iter, b);
+    else if (accel == ACCEL_BVH) hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_BVH, BS>), grid, dim3(BS), 0, st, kp, iter, b);
     else if (accel == ACCEL_GRID_FAST)
         hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_GRID_FAST, BS>), grid, dim3(BS), 0, st, kp, iter, b);
     else hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_GRID, BS>), grid, dim3(BS), 0, st, kp, iter, b);
 }
 
-void Renderer::launchBounce(bool first, dim3 grid, int iter, int b) {
+void Renderer::launchBounce(bool first, dim3 grid, int iter, int b, int accel) {
     switch (kp.chunk) {
         case 64:
-            if (first) launch_bounce_bs<true, 64>(cfg.accel, grid, stream, kp, iter, b);
-            else launch_bounce_bs<false, 64>(cfg.accel, grid, stream, kp, iter, b);
+            if (first) launch_bounce_bs<true, 64>(accel, grid, stream, kp, iter, b);
+            else launch_bounce_bs<false, 64>(accel, grid, stream, kp, iter, b);
             break;
         case 128:
-            if (first) launch_bounce_bs<true, 128>(cfg.accel, grid, stream, kp, iter, b);
-            else launch_bounce_bs<false, 128>(cfg.accel, grid, stream, kp, iter, b);
+            if (first) launch_bounce_bs<true, 128>(accel, grid, stream, kp, iter, b);
+            else launch_bounce_bs<false, 128>(accel, grid, stream, kp, iter, b);
             break;
         default:
-            if (first) launch_bounce_bs<true, 256>(cfg.accel, grid, stream, kp, iter, b);
-            else launch_bounce_bs<false, 256>(cfg.accel, grid, stream, kp, iter, b);
+            if (first) launch_bounce_bs<true, 256>(accel, grid, stream, kp, iter, b);
+            else launch_bounce_bs<false, 256>(accel, grid, stream, kp, iter, b);
             break;
     }
 }
@@ -992,7 +1157,18 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
         for (int b = 0; b < passes; b++) {
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
-            launchBounce(b == 0, grid, iter, b);
+            if (b > 0 && split_trace) {
+                hipLaunchKernelGGL(k_trace_bvh<64>, dim3((unsigned)trace_blocks), dim3(64), 0, stream, kp, b);
+                PT_HIP(hipGetLastError());
+                if (profiling) {
+                    hipEventRecord(e1, stream);
+                    trace_events.push_back({e0, e1});
+                    hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream);
+                }
+                launchBounce(false, grid, iter, b, kAccelHitBuffer);
+            } else {
+                launchBounce(b == 0, grid, iter, b, cfg.accel);
+            }
             PT_HIP(hipGetLastError());
             if (profiling) {
                 hipEventRecord(e1, stream);
@@ -1036,6 +1212,14 @@ int Renderer::kernelStats(KernelStats* out) {
         hipEventDestroy(ev.first); hipEventDestroy(ev.second);
     }
     first_events.clear();
+    for (auto& ev : trace_events) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev.first, ev.second);
+        stats.trace_ms += ms;
+        stats.trace_launches++;
+        hipEventDestroy(ev.first); hipEventDestroy(ev.second);
+    }
+    trace_events.clear();
     for (auto& ev : scan_events) {
         float ms = 0;
         hipEventElapsedTime(&ms, ev.first, ev.second);
@@ -1060,11 +1244,11 @@ long long Renderer::segments() {
 
 int Renderer::segmentsPerBounce(long long* out, int n) {
     if (!allocated) { last_error = "not allocated"; return -1; }
-    unsigned long long v[4 + kMaxBounceCounters];
+    unsigned long long v[8 + kMaxBounceCounters];
     PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n && i < kMaxBounceCounters + 3; i++) out[i] = (long long)v[1 + i];
-    for (int i = kMaxBounceCounters + 3; i < n; i++) out[i] = 0;
+    for (int i = 0; i < n && i < kMaxBounceCounters + 7; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters + 7; i < n; i++) out[i] = 0;
     return 0;
 }
 
@@ -1177,6 +1361,8 @@ void Renderer::free() {
     for (auto& ev : bounce_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto& ev : first_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto& ev : scan_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    for (auto& ev : trace_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    trace_events.clear();
     bounce_events.clear();
     first_events.clear();
     scan_events.clear();

@@ -3,6 +3,7 @@
 rounds on one device; cdna_hip_programming.md §5.4 rule 24).
 
     python scripts/ab.py --variants bvh:256 bvh:128 bvh:64 grid:256 --rounds 5 --steps 8
+    python scripts/ab.py --variants bvh:64:PT_TRACE_SPLIT=0 bvh:64:PT_TRACE_REFILL=8   (env read at allocateOnGPU)
 """
 import argparse
 import json
@@ -34,7 +35,11 @@ def main():
     scenes = {}
     rs = {}
     for v in a.variants:
-        accel, block = v.split(":")
+        parts = v.split(":")
+        accel, block = parts[0], parts[1]
+        env = dict(kv.split("=") for kv in parts[2].split(",")) if len(parts) > 2 else {}
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)          # read by allocateOnGPU
         acc = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[accel]
         if acc not in scenes:
             s = P.Scene(path)
@@ -43,6 +48,11 @@ def main():
         cfg = P.RenderConfig(width=a.width, height=a.height, max_bounces=a.bounces, accel=acc, block=int(block))
         r = P.Renderer(cfg)
         r.allocateOnGPU(scenes[acc])
+        for k, old in saved.items():
+            if old is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old
         r.renderLoop(1000, 2)          # warm + primary cache
         rs[v] = r
     times = {v: [] for v in a.variants}
@@ -60,9 +70,14 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
-        diag = rs[v].segments_per_bounce(67)[64:67]
+        allc = rs[v].segments_per_bounce(70)
+        diag = allc[64:67]
         if any(diag):
             out[v]["diag_tier2_t1overflow_fallback"] = diag
+        if allc[69]:
+            out[v]["nodes_per_traversal"] = round(allc[67] / allc[69], 2)
+            out[v]["tris_per_traversal"] = round(allc[68] / allc[69], 2)
+            out[v]["traversals_per_segment"] = round(allc[69] / rs[v].segments(), 3)
     print(json.dumps(out, indent=1))
 
 
