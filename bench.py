@@ -238,23 +238,39 @@ def main():
         samples = world * K * npix / elapsed
         roof = None
         if stats and stats["bounce_ms"] > 0:
-            # Dominant kernel: k_bounce<secondary> (bounces >= 1).  Algorithmic HBM bytes per ray
-            # segment entering bounce b >= 1: 48 B ray-state gather; a survivor writes 48 B of
-            # compacted state, a terminated ray read-modify-writes its 12 B accumulator pixel.
-            # Scene data (BVH nodes / triangles, ~7 MB) is cache-resident and not counted.
+            # Dominant kernel on bounces >= 1 (see DESIGN.md "Kernels and their rooflines").
+            # Fused k_bounce: per ray segment entering bounce b >= 1, 48 B ray-state gather; a
+            # survivor writes 48 B of compacted state, a terminated ray read-modify-writes its
+            # 12 B accumulator pixel.  Split path (ACCEL_BVH): k_trace_bvh reads o, d (32 B) and
+            # writes the 20 B hit record per segment; the shading pass reads ray + hit (68 B)
+            # and writes as above.  Scene data (BVH nodes / triangles) is cache-resident and not
+            # counted.
             nb = [x for x in per_bounce]
-            nbytes = 0.0
+            shade_bytes = 0.0
+            trace_bytes = 0.0
+            split = stats.get("trace_launches", 0) > 0
             for b in range(1, len(nb)):
                 nxt = nb[b + 1] if b + 1 < len(nb) else 0
-                nbytes += 48.0 * nb[b] + 48.0 * nxt + 24.0 * (nb[b] - nxt)
-            launches = max(stats["bounce_launches"], 1)
-            achieved = nbytes / (stats["bounce_ms"] / 1e3) / 1e9
-            kname = f"k_bounce<false,{args.accel}>"
+                shade_bytes += (68.0 if split else 48.0) * nb[b] + 48.0 * nxt + 24.0 * (nb[b] - nxt)
+                trace_bytes += 52.0 * nb[b]
+            shade = {"launches": stats["bounce_launches"],
+                     "avg_launch_ms": round(stats["bounce_ms"] / max(stats["bounce_launches"], 1), 4)}
+            if split:
+                kname = "k_trace_bvh" if args.accel == "bvh" else "k_trace_gf"
+                nbytes, kms, launches = trace_bytes, stats["trace_ms"], max(stats["trace_launches"], 1)
+                shade["kernel"] = "k_bounce<false,hitbuf>"
+                shade["achieved_gbs"] = round(shade_bytes / (stats["bounce_ms"] / 1e3) / 1e9, 2)
+            else:
+                kname = f"k_bounce<false,{args.accel}>"
+                nbytes, kms, launches = shade_bytes, stats["bounce_ms"], max(stats["bounce_launches"], 1)
+                shade = None
+            achieved = nbytes / (kms / 1e3) / 1e9
             traffic = load_pmc(kname, workload_key)
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "kernel": kname, "algorithmic_bytes_per_launch": round(nbytes / launches),
-                    "avg_launch_ms": round(stats["bounce_ms"] / launches, 4), "launches": stats["bounce_launches"],
+                    "avg_launch_ms": round(kms / launches, 4), "launches": launches,
+                    "shading_pass": shade,
                     "first_bounce_avg_ms": round(stats["first_ms"] / max(stats["first_launches"], 1), 4),
                     "scan_avg_ms": round(stats["scan_ms"] / max(stats["scan_launches"], 1), 4)}
         cpu = None
@@ -268,8 +284,7 @@ def main():
             "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "samples_per_sec": round(samples, 1),
-            "config": {"workload": workload_name(args)
-                                   + (" [metallic variant]" if args.metallic else ""),
+            "config": {"workload": workload_name(args),
                        "triangles": ntri, "width": cfg.width, "height": cfg.height, "bounces": cfg.max_bounces,
                        "spp_per_step": 1, "accel": args.accel,
                        "results": "bit-identical to the reference algorithm (oracle-checked)"

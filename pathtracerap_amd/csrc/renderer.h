@@ -61,8 +61,11 @@ struct KParams {
     int hs_pool_blocks;
     float4* hit4;                       // split trace/shade (ACCEL_BVH): per-slot dist, normal
     int* hitm;                          // per-slot model
-    int* trace_next;                    // persistent trace work counter, reset by k_scan
+    int* trace_next;                    // persistent trace: next unclaimed source block, reset by k_scan
     int trace_refill;                   // refill a wave's idle lanes once this many are idle
+    int* defer_slots;                   // grid_fast: slots k_trace_gf handed to k_trace_deferred
+    int* defer_count;                   // reset by k_scan
+    int trace_flags;                    // k_trace_bvh variant: 1 LDS model records, 2 leaf steps, 4 block claims
 };
 
 constexpr int kMaxBounceCounters = 64;
@@ -99,6 +102,7 @@ public:
 
 private:
     int launchPrimary();
+    void launchTrace(int b);
     void launchBounce(bool first, dim3 grid, int iter, int b, int accel);
     int fail(hipError_t e, const char* what);
     void freeBuffers();

@@ -31,6 +31,9 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP
 #define PT_HITCAP 6
 #endif
+#ifndef PT_HITCAP_TRACE
+#define PT_HITCAP_TRACE 4     // hit-set entries per lane in the persistent grid_fast trace (overflow -> deferred)
+#endif
 #ifndef PT_MINWAVES
 #define PT_MINWAVES 5
 #endif
@@ -367,83 +370,122 @@ struct WalkResult {
 // depend on V, so V is a hit voxel iff some member's box contains V.  The
 // reference keeps the first strict minimum in test order (voxel order, then
 // ascending index inside a list): the lexicographic minimum of (t, step, index).
-template <int HSTRIDE>
-__device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
-                                  const int4* __restrict__ hs, int nh, float tmin) {
+// Split into init + one voxel per step so the persistent trace kernel can
+// interleave walks with other lanes' traversal steps.
+struct Walk {
+    int ix, iy, iz, k;
+    f3 tmax, delta;
+    int ul, uh;                    // union of the members' voxel boxes (packed 10 bits/axis)
+    int c;                         // last hit voxel (packed)
+    unsigned long long tested;
+    float bt;
+    int bk, bi;
+    bool hit;
+};
+
+__device__ __forceinline__ void walk_init(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, Walk& w) {
     const int GX = p.gdim[0], GY = p.gdim[1], GZ = p.gdim[2];
     int ix = f2i_sat(absr(pt.x - M.bbox[0] + kEps) / M.vw[0]);
     int iy = f2i_sat(absr(pt.y - M.bbox[1] + kEps) / M.vw[1]);
     int iz = f2i_sat(absr(pt.z - M.bbox[2] + kEps) / M.vw[2]);
-    ix = ix < 0 ? 0 : (ix > GX - 1 ? GX - 1 : ix);
-    iy = iy < 0 ? 0 : (iy > GY - 1 ? GY - 1 : iy);
-    iz = iz < 0 ? 0 : (iz > GZ - 1 ? GZ - 1 : iz);
-    f3 tmax = mk3(kFMax, kFMax, kFMax), delta = mk3(kFMax, kFMax, kFMax);
-    const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
-    const int ox = d.x > 0.0f ? GX : -1, oy = d.y > 0.0f ? GY : -1, oz = d.z > 0.0f ? GZ : -1;
-    const int nx = d.x > 0.0f ? ix + 1 : ix, ny = d.y > 0.0f ? iy + 1 : iy, nz = d.z > 0.0f ? iz + 1 : iz;
+    w.ix = ix < 0 ? 0 : (ix > GX - 1 ? GX - 1 : ix);
+    w.iy = iy < 0 ? 0 : (iy > GY - 1 ? GY - 1 : iy);
+    w.iz = iz < 0 ? 0 : (iz > GZ - 1 ? GZ - 1 : iz);
+    w.tmax = mk3(kFMax, kFMax, kFMax);
+    w.delta = mk3(kFMax, kFMax, kFMax);
+    const int nx = d.x > 0.0f ? w.ix + 1 : w.ix, ny = d.y > 0.0f ? w.iy + 1 : w.iy, nz = d.z > 0.0f ? w.iz + 1 : w.iz;
     const float px = M.bbox[0] + (float)nx * M.vw[0];
     const float py = M.bbox[1] + (float)ny * M.vw[1];
     const float pz = M.bbox[2] + (float)nz * M.vw[2];
-    if (d.x != 0) { delta.x = absr(M.vw[0] * inv.x); tmax.x = (px - pt.x) * inv.x; }
-    if (d.y != 0) { delta.y = absr(M.vw[1] * inv.y); tmax.y = (py - pt.y) * inv.y; }
-    if (d.z != 0) { delta.z = absr(M.vw[2] * inv.z); tmax.z = (pz - pt.z) * inv.z; }
-    // union of the members' voxel boxes: outside it no voxel is a hit voxel
+    if (d.x != 0) { w.delta.x = absr(M.vw[0] * inv.x); w.tmax.x = (px - pt.x) * inv.x; }
+    if (d.y != 0) { w.delta.y = absr(M.vw[1] * inv.y); w.tmax.y = (py - pt.y) * inv.y; }
+    if (d.z != 0) { w.delta.z = absr(M.vw[2] * inv.z); w.tmax.z = (pz - pt.z) * inv.z; }
+    w.k = 0;
+    w.c = 0;
+    w.tested = 0;
+    w.bt = kFMax;
+    w.bk = -1;
+    w.bi = -1;
+    w.hit = false;
+}
+
+template <int HSTRIDE>
+__device__ __forceinline__ void walk_union(const int4* __restrict__ hs, int nh, Walk& w) {
     int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
     for (int h = 0; h < nh; h++) {
         const int4 e = hs[h * HSTRIDE];
         ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
         uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
     }
-    const unsigned long long all = nh >= 64 ? ~0ull : ((1ull << nh) - 1ull);
-    int cx = 0, cy = 0, cz = 0;
-    bool hit = false;
-    unsigned long long tested = 0;
-    float bt = kFMax;
-    int bk = -1, bi = -1;
-    for (int k = 0;; k++) {
-        bool vhit = false;
-        if (ix >= ulx && ix <= uhx && iy >= uly && iy <= uhy && iz >= ulz && iz <= uhz) {
-            for (int h = 0; h < nh; h++) {
-                const int4 e = hs[h * HSTRIDE];
-                if (vbox_has(e.z, e.w, ix, iy, iz)) {
-                    vhit = true;
-                    if (!((tested >> h) & 1ull)) {
-                        tested |= 1ull << h;
-                        const float t = __int_as_float(e.x);
-                        if (t < bt || (t == bt && (k < bk || (k == bk && e.y < bi)))) { bt = t; bk = k; bi = e.y; }
-                    }
+    w.ul = ulx | (uly << 10) | (ulz << 20);
+    w.uh = uhx | (uhy << 10) | (uhz << 20);
+}
+
+// One voxel of the walk; returns true when the walk has stopped.
+template <int HSTRIDE>
+__device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __restrict__ hs, int nh, float tmin,
+                                          Walk& w) {
+    const int ulx = w.ul & 1023, uly = (w.ul >> 10) & 1023, ulz = (w.ul >> 20) & 1023;
+    const int uhx = w.uh & 1023, uhy = (w.uh >> 10) & 1023, uhz = (w.uh >> 20) & 1023;
+    const int ix = w.ix, iy = w.iy, iz = w.iz, k = w.k;
+    bool vhit = false;
+    if (ix >= ulx && ix <= uhx && iy >= uly && iy <= uhy && iz >= ulz && iz <= uhz) {
+        for (int h = 0; h < nh; h++) {
+            const int4 e = hs[h * HSTRIDE];
+            if (vbox_has(e.z, e.w, ix, iy, iz)) {
+                vhit = true;
+                if (!((w.tested >> h) & 1ull)) {
+                    w.tested |= 1ull << h;
+                    const float t = __int_as_float(e.x);
+                    if (t < w.bt || (t == w.bt && (k < w.bk || (k == w.bk && e.y < w.bi)))) { w.bt = t; w.bk = k; w.bi = e.y; }
                 }
             }
         }
-        if (vhit) { cx = ix; cy = iy; cz = iz; hit = true; }
-        // Exact shortcuts: once a minimum-t member (or every member) is tested the
-        // result and the return value are final; once the monotone walk has passed
-        // the union box along an axis it enters no member's box again.
-        if (tested == all || (bk >= 0 && bt == tmin)) break;
-        if ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz)) break;
-        if (hit && (iabs(cx - ix) > 2 || iabs(cy - iy) > 2 || iabs(cz - iz) > 2)) break;
-        if (tmax.x < tmax.y && tmax.x < tmax.z) {
-            ix += sx;
-            if (ix == ox || tmax.x >= kFMax) break;
-            tmax.x += delta.x;
-        } else if (tmax.y < tmax.z) {
-            iy += sy;
-            if (iy == oy || tmax.y >= kFMax) break;
-            tmax.y += delta.y;
-        } else {
-            iz += sz;
-            if (iz == oz || tmax.z >= kFMax) break;
-            tmax.z += delta.z;
-        }
     }
-    WalkResult w;
-    w.hit = hit;
-    w.t = bt;
-    w.tri = bi;
-    w.has_best = bk >= 0;
-    w.final_min = bk >= 0 && bt == tmin;
-    w.tw = t_box + fminf(fminf(tmax.x, tmax.y), tmax.z);
-    return w;
+    if (vhit) { w.c = ix | (iy << 10) | (iz << 20); w.hit = true; }
+    // Exact shortcuts: once a minimum-t member (or every member) is tested the
+    // result and the return value are final; once the monotone walk has passed
+    // the union box along an axis it enters no member's box again.
+    const unsigned long long all = nh >= 64 ? ~0ull : ((1ull << nh) - 1ull);
+    if (w.tested == all || (w.bk >= 0 && w.bt == tmin)) return true;
+    const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
+    if ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz)) return true;
+    if (w.hit) {
+        const int cx = w.c & 1023, cy = (w.c >> 10) & 1023, cz = (w.c >> 20) & 1023;
+        if (iabs(cx - ix) > 2 || iabs(cy - iy) > 2 || iabs(cz - iz) > 2) return true;
+    }
+    w.k = k + 1;
+    if (w.tmax.x < w.tmax.y && w.tmax.x < w.tmax.z) {
+        w.ix = ix + sx;
+        if (w.ix == (d.x > 0.0f ? p.gdim[0] : -1) || w.tmax.x >= kFMax) return true;
+        w.tmax.x += w.delta.x;
+    } else if (w.tmax.y < w.tmax.z) {
+        w.iy = iy + sy;
+        if (w.iy == (d.y > 0.0f ? p.gdim[1] : -1) || w.tmax.y >= kFMax) return true;
+        w.tmax.y += w.delta.y;
+    } else {
+        w.iz = iz + sz;
+        if (w.iz == (d.z > 0.0f ? p.gdim[2] : -1) || w.tmax.z >= kFMax) return true;
+        w.tmax.z += w.delta.z;
+    }
+    return false;
+}
+
+template <int HSTRIDE>
+__device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
+                                  const int4* __restrict__ hs, int nh, float tmin) {
+    Walk w;
+    walk_init(p, M, d, inv, pt, w);
+    walk_union<HSTRIDE>(hs, nh, w);
+    while (!walk_step<HSTRIDE>(p, d, hs, nh, tmin, w)) {}
+    WalkResult r;
+    r.hit = w.hit;
+    r.t = w.bt;
+    r.tri = w.bi;
+    r.has_best = w.bk >= 0;
+    r.final_min = w.bk >= 0 && w.bt == tmin;
+    r.tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
+    return r;
 }
 
 // Overflow tiers of grid_hitset: bounded, then unbounded collection into a
@@ -684,19 +726,40 @@ __device__ __forceinline__ int slot_source(const KParams& p, int j) {
 // Persistent BLAS trace for one bounce (ACCEL_BVH): computeRaySceneIntersectionKernel
 // (Renderer.cpp:363-409) for every live slot, result-identical to
 // intersect_scene<ACCEL_BVH>, written to the hit buffer the shading pass reads.
-// Each lane runs its own ray through (model select -> node visits) one step
-// per loop iteration and fetches a new slot from a global counter when its
-// ray is done, so a wave's lanes stay busy instead of idling behind the
-// wave's longest ray (secondary rays are incoherent).  Every wave exits once
-// the counter passes n and its lanes are idle.
-template <int BS>
+// Each lane runs its own ray through (model select -> node visits -> leaf
+// triangles) one step per loop iteration and takes a new ray when its ray is
+// done, so a wave's lanes stay busy instead of idling behind the wave's
+// longest ray (secondary rays are incoherent).  Work is claimed per source
+// block of the previous bounce (one atomic per <= chunk rays): block b's
+// survivors sit at [b*chunk, b*chunk + cnt_b) and own dense slots
+// [blk_off[b], blk_off[b] + cnt_b), so no slot->source search is needed.
+// Every wave exits once all blocks are claimed and its lanes are idle.
+constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
+
+// F (compile-time variant): 1 = model records in LDS, 2 = leaf triangles as
+// their own steps, 4 = claim source blocks (else: claim slots + search).
+template <int BS, int F>
 __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     __shared__ int s_stack[kStack * BS];
+    __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
-    const int n = p.n_live[bounce];
+    const bool lds_models = (F & 1) && p.nmodels <= kLdsModels;
+    if (lds_models) {
+        const int* src = reinterpret_cast<const int*>(p.models);
+        int* dst = reinterpret_cast<int*>(s_models);
+        const int nw = p.nmodels * (int)(sizeof(ModelRec) / 4);
+        for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
+        __syncthreads();
+    }
+    const ModelRec* models = lds_models ? s_models : p.models;
+    const int n_prev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
+    const int CH = p.chunk;
+    const int nb = (n_prev + CH - 1) / CH;          // source blocks written by the previous bounce
     const int in_buf = (bounce + 1) & 1;
     const int lane = threadIdx.x & 63;
-    // lane state: 0 = needs a ray, 1 = select next model, 2 = traversing, 3 = no more rays
+    constexpr bool leaf_state = (F & 2) != 0;
+    const int n = p.n_live[bounce];
+    // lane state: 0 = needs a ray, 1 = select next model, 2 = node visits, 4 = leaf triangles, 3 = no more rays
     int state = 0;
     int j = -1;
     f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
@@ -704,12 +767,246 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     int gmodel = -1, gtri = -1, im = -1;
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0);
     int cur = 0, sp = 0, best_tri = -1, n_tris = 0;
+    int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0;    // pending leaves: [lf_i, lf_e) then [lf2_i, lf2_e)
+    int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
     bool any = false, exhausted = false;
+    int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // wave's claimed source block (uniform)
     for (unsigned iters = 0;; iters++) {
-        // refill idle lanes (wave-aggregated atomic) once enough are idle
+        unsigned long long idle = __ballot(state == 0);
+        const unsigned long long busy = __ballot(state != 0 && state != 3);
+        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+            if (F & 4) {
+                for (int guard = 0; guard < 4 && idle; guard++) {
+                    if (q_pos >= q_cnt) {                           // claim the next non-empty source block
+                        int b = 0;
+                        if (lane == 0) b = atomicAdd(p.trace_next, 1);
+                        b = __shfl(b, 0);
+                        if (b >= nb) { exhausted = true; break; }
+                        q_b = b; q_pos = 0; q_cnt = p.blk_cnt[b]; q_off = p.blk_off[b];
+                        continue;
+                    }
+                    const int take = min(__popcll(idle), q_cnt - q_pos);
+                    const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+                    if (state == 0 && rank < take) {
+                        const int src = q_b * CH + q_pos + rank;
+                        j = q_off + q_pos + rank;
+                        const float4 a = p.ray[in_buf][0][src];
+                        const float4 b = p.ray[in_buf][1][src];
+                        ow = mk3(a.x, a.y, a.z);
+                        dw = mk3(b.x, b.y, b.z);
+                        winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                        dlen = sqrtf(dot(dw, dw));
+                        gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
+                        state = 1;
+                    }
+                    q_pos += take;
+                    idle = __ballot(state == 0);
+                }
+            } else {
+                const int cnt = __popcll(idle);
+                const int leader = __ffsll((long long)idle) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(p.trace_next, cnt);
+                base = __shfl(base, leader);
+                if (base + cnt >= n) exhausted = true;
+                if (state == 0) {
+                    j = base + __popcll(idle & ((1ull << lane) - 1ull));
+                    if (j < n) {
+                        const int src = slot_source(p, j);
+                        const float4 a = p.ray[in_buf][0][src];
+                        const float4 b = p.ray[in_buf][1][src];
+                        ow = mk3(a.x, a.y, a.z);
+                        dw = mk3(b.x, b.y, b.z);
+                        winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                        dlen = sqrtf(dot(dw, dw));
+                        gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
+                        state = 1;
+                    } else {
+                        state = 3;
+                    }
+                }
+            }
+        }
+        if (exhausted && state == 0) state = 3;
+        if (__ballot(state != 3) == 0) break;
+        if (iters > (1u << 26)) {                       // safety net: never spin forever
+            if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
+            break;
+        }
+        // Phase scheduling (F & 8): one step kind per iteration -- the one most
+        // lanes are waiting in -- so the wave never pays for three partly used blocks.
+        int phase = 7;
+        if (F & 8) {
+            const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
+                      c4 = __popcll(__ballot(state == 4));
+            phase = (c2 >= c4 && c2 >= c1) ? 2 : (c4 >= c1 ? 4 : 1);
+        }
+        if ((phase & 1) && state == 1) {                // advance to the next model that survives culling
+            for (;;) {
+                im++;
+                if (im >= p.nmodels) {
+                    Hit h;
+                    h.dist = kFMax; h.n = mk3(0, 0, 0); h.model = -1;
+                    if (gdist < kFMax) {
+                        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
+                        h.dist = gdist;
+                        h.model = gmodel;
+                        h.n = normalize(xform_normal9(models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
+                    }
+                    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+                    p.hitm[j] = h.model;
+                    state = 0;
+                    break;
+                }
+                const ModelRec& M = models[im];
+                if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                o = xform12(M.w2m, ow, 1.0f);
+                d = normalize(xform12(M.w2m, dw, 0.0f));
+                ninv = node_inv(mk3(1 / d.x, 1 / d.y, 1 / d.z));
+                cur = M.bvh_root;
+                sp = 0;
+                best = kFMax;
+                best_tri = -1;
+                any = false;
+                state = 2;
+                break;
+            }
+        }
+        bool model_done = false;
+        if ((phase & 4) && state == 4) {                // one leaf triangle per iteration
+            const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
+            const int it = __float_as_int(A.w);
+            float t;
+            if (tri_test_rec(A, B, C, o, d, t)) {
+                any = true;
+                if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+            }
+            lf_i++;
+            if (lf_i == lf_e) {
+                if (lf2_i < lf2_e) {                    // second leaf child
+                    lf_i = lf2_i; lf_e = lf2_e;
+                    lf2_i = lf2_e = 0;
+                } else if (lf_next >= 0) {
+                    cur = lf_next;
+                    state = 2;
+                } else if (sp == 0) {
+                    model_done = true;
+                } else {
+                    sp--;
+                    cur = stack[sp * BS];
+                    state = 2;
+                }
+            }
+        } else if ((phase & 2) && state == 2) {
+            if (!leaf_state) {
+                model_done = bvh_step<BS>(p, o, d, ninv, cur, sp, stack, best, best_tri, any, n_tris);
+            } else {
+                // node visit; hit leaf children become pending leaves (tested one
+                // triangle per iteration, in the order bvh_step tests them)
+                const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+                const float4 q0 = nodes[4 * cur + 0];
+                const float4 q1 = nodes[4 * cur + 1];
+                const float4 q2 = nodes[4 * cur + 2];
+                const float4 q3 = nodes[4 * cur + 3];
+                const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+                const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+                const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+                const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+                float tn0, tf0, tn1, tf1;
+                node_slab(lo0, hi0, o, ninv, tn0, tf0);
+                node_slab(lo1, hi1, o, ninv, tn1, tf1);
+                const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
+                const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
+                const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
+                const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
+                // next node after the leaves: same rule as bvh_step
+                int next = -1;
+                if (i0 && i1) {
+                    const bool first0 = tn0 <= tn1;
+                    stack[sp * BS] = first0 ? link1 : link0;
+                    sp++;
+                    next = first0 ? link0 : link1;
+                } else if (i0) {
+                    next = link0;
+                } else if (i1) {
+                    next = link1;
+                }
+                if (l0 && l1) {                 // leaf 0, then leaf 1, then `next`
+                    lf_i = link0; lf_e = link0 + cnt0;
+                    lf2_i = link1; lf2_e = link1 + cnt1;
+                    lf_next = next;
+                    state = 4;
+                } else if (l0 || l1) {
+                    lf_i = l0 ? link0 : link1;
+                    lf_e = lf_i + (l0 ? cnt0 : cnt1);
+                    lf2_i = lf2_e = 0;
+                    lf_next = next;
+                    state = 4;
+                } else if (next >= 0) {
+                    cur = next;
+                } else if (sp == 0) {
+                    model_done = true;
+                } else {
+                    sp--;
+                    cur = stack[sp * BS];
+                }
+            }
+        }
+        if (model_done) {
+            if (any) {
+                const float dd = model_hit_dist(models[im], o, d, best, ow);
+                if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
+            }
+            state = 1;
+        }
+    }
+}
+
+// Persistent grid_fast trace for one bounce: computeRayGridIntersection
+// results (Renderer.cpp:238-360, via the BLAS hit set as in grid_hitset) for
+// every live slot, written to the hit buffer.  Per lane: model select ->
+// bounded collection (node visits and leaf triangles as separate steps) ->
+// DDA walk (one voxel per step).  Rays that need more than tier 1 in LDS
+// (hit-set overflow, or a walk that is not provably exact) are deferred to
+// k_trace_deferred, which recomputes them with every tier.
+constexpr int kHitCapT = PT_HITCAP_TRACE;
+
+template <int BS, int F>
+__global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
+    __shared__ int s_stack[kStack * BS];
+    __shared__ int4 s_hs[kHitCapT * BS];
+    int* stack = s_stack + threadIdx.x;
+    int4* hs = s_hs + threadIdx.x;
+    const int n = p.n_live[bounce];
+    const int in_buf = (bounce + 1) & 1;
+    const int lane = threadIdx.x & 63;
+    // lane state: 0 needs a ray, 1 select model, 2 node visit, 4 leaf triangle, 5 walk, 3 no more rays
+    int state = 0;
+    int j = -1;
+    f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
+    float dlen = 0.0f, gdist = kFMax;
+    int gmodel = -1, gtri = -1, im = -1;
+    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), inv = mk3(0, 0, 0), ninv = mk3(0, 0, 0);
+    float t_box = 0.0f, tmin = kFMax, margin = 0.0f;
+    int cur = 0, sp = 0, nh = 0;
+    int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
+    Walk w;
+    w.ix = w.iy = w.iz = w.k = w.ul = w.uh = w.c = w.bk = w.bi = 0;
+    w.tmax = w.delta = mk3(0, 0, 0);
+    w.tested = 0; w.bt = kFMax; w.hit = false;
+    bool exhausted = false;
+    unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
+    for (unsigned iters = 0;; iters++) {
         const unsigned long long idle = __ballot(state == 0);
-        const unsigned long long busy = __ballot(state == 1 || state == 2);
+        const unsigned long long busy = __ballot(state != 0 && state != 3);
+        if (p.debug & 16) {
+            st_iter++;
+            st_node += __popcll(__ballot(state == 2));
+            st_leaf += __popcll(__ballot(state == 4));
+            st_walk += __popcll(__ballot(state == 5));
+            st_sel += __popcll(__ballot(state == 1));
+        }
         if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
@@ -740,8 +1037,18 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
             if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
             break;
         }
-        if (state == 1) {                               // advance to the next model that survives culling
+        int phase = 15;
+        if (F & 8) {
+            const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
+                      c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5));
+            phase = 2; int cm = c2;
+            if (c4 > cm) { phase = 4; cm = c4; }
+            if (c5 > cm) { phase = 8; cm = c5; }
+            if (c1 > cm) { phase = 1; cm = c1; }
+        }
+        if ((phase & 1) && state == 1) {
             for (;;) {
+                if (p.debug & 16) atomicAdd(p.segments + 13 + kMaxBounceCounters, 1ull);
                 im++;
                 if (im >= p.nmodels) {
                     const Hit h = make_hit(p, gdist, gmodel, gtri);
@@ -751,28 +1058,164 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                     break;
                 }
                 const ModelRec& M = p.models[im];
-                if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
-                ninv = node_inv(mk3(1 / d.x, 1 / d.y, 1 / d.z));
+                inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+                if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
+                const f3 pt = o + d * t_box;
+                if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
+                ninv = node_inv(inv);
+                margin = 2.0f * M.reach;
                 cur = M.bvh_root;
                 sp = 0;
-                best = kFMax;
-                best_tri = -1;
-                any = false;
+                nh = 0;
+                tmin = kFMax;
                 state = 2;
                 break;
             }
         }
-        if (state == 2) {
-            if (bvh_step<BS>(p, o, d, ninv, cur, sp, stack, best, best_tri, any, n_tris)) {
-                if (any) {
-                    const float dd = model_hit_dist(p.models[im], o, d, best, ow);
-                    if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
+        bool collected = false;
+        if ((phase & 4) && state == 4) {                // one leaf triangle of the bounded collection
+            const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
+            float t;
+            if (tri_test_rec(A, B, C, o, d, t)) {
+                if (t < tmin) tmin = t;
+                if (!(t > tmin + margin)) {
+                    if (nh == kHitCapT) {                   // drop members now beyond the bound
+                        int wn = 0;
+                        for (int q = 0; q < nh; q++) {
+                            const int4 e = hs[q * BS];
+                            if (!(__int_as_float(e.x) > tmin + margin)) hs[(wn++) * BS] = e;
+                        }
+                        nh = wn;
+                    }
+                    if (nh == kHitCapT) {                   // overflow: defer the whole ray
+                        p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                        state = 0;
+                    } else {
+                        hs[nh * BS] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
+                                                __float_as_int(C.w));
+                        nh++;
+                    }
                 }
-                state = 1;
+            }
+            if (state == 4) {
+                lf_i++;
+                if (lf_i == lf_e) {
+                    if (lf2_i < lf2_e) {
+                        lf_i = lf2_i; lf_e = lf2_e;
+                        lf2_i = lf2_e = 0;
+                    } else if (lf_next >= 0) {
+                        cur = lf_next;
+                        state = 2;
+                    } else if (sp == 0) {
+                        collected = true;
+                    } else {
+                        sp--;
+                        cur = stack[sp * BS];
+                        state = 2;
+                    }
+                }
+            }
+        } else if ((phase & 2) && state == 2) {         // one node of the bounded collection
+            const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+            const float4 q0 = nodes[4 * cur + 0];
+            const float4 q1 = nodes[4 * cur + 1];
+            const float4 q2 = nodes[4 * cur + 2];
+            const float4 q3 = nodes[4 * cur + 3];
+            const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+            const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+            const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+            const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+            float tn0, tf0, tn1, tf1;
+            node_slab(lo0, hi0, o, ninv, tn0, tf0);
+            node_slab(lo1, hi1, o, ninv, tn1, tf1);
+            const float bound = tmin + margin;
+            const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bound;
+            const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bound;
+            const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
+            const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
+            int next = -1;
+            if (i0 && i1) {
+                const bool first0 = tn0 <= tn1;
+                stack[sp * BS] = first0 ? link1 : link0;
+                sp++;
+                next = first0 ? link0 : link1;
+            } else if (i0) {
+                next = link0;
+            } else if (i1) {
+                next = link1;
+            }
+            if (l0 || l1) {
+                lf_i = l0 ? link0 : link1;
+                lf_e = lf_i + (l0 ? cnt0 : cnt1);
+                lf2_i = (l0 && l1) ? link1 : 0;
+                lf2_e = (l0 && l1) ? link1 + cnt1 : 0;
+                lf_next = next;
+                state = 4;
+            } else if (next >= 0) {
+                cur = next;
+            } else if (sp == 0) {
+                collected = true;
+            } else {
+                sp--;
+                cur = stack[sp * BS];
             }
         }
+        if (collected) {
+            if (nh == 0) {
+                state = 1;                              // no accepted triangle on the ray: no hit voxel
+            } else {
+                walk_init(p, p.models[im], d, inv, o + d * t_box, w);
+                walk_union<BS>(hs, nh, w);
+                state = 5;
+            }
+        } else if ((phase & 8) && state == 5) {
+            if (walk_step<BS>(p, d, hs, nh, tmin, w)) {
+                const ModelRec& M = p.models[im];
+                const bool final_min = w.bk >= 0 && w.bt == tmin;
+                const float tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
+                if (final_min || tw < tmin + M.reach) {
+                    if (w.hit) {
+                        const float best = w.bk >= 0 ? w.bt : kFMax;
+                        const float dd = model_hit_dist(M, o, d, best, ow);
+                        if (gdist > dd) { gdist = dd; gmodel = im; gtri = w.bk >= 0 ? w.bi : -1; }
+                    }
+                    state = 1;
+                } else {                                // tier 1 not provably exact: defer the ray
+                    p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                    state = 0;
+                }
+            }
+        }
+    }
+    if ((p.debug & 16) && lane == 0) {
+        atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
+        atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
+        atomicAdd(p.segments + 11 + kMaxBounceCounters, st_walk);
+        atomicAdd(p.segments + 12 + kMaxBounceCounters, st_sel);
+    }
+}
+
+// Rays k_trace_gf deferred: the full grid_hitset tiers (LDS, global pool,
+// list-walking DDA), one lane per ray.
+__global__ __launch_bounds__(kBlock) void k_trace_deferred(KParams p, int bounce) {
+    __shared__ int s_stack[kStack * kBlock];
+    __shared__ int4 s_hs[kHitCap * kBlock];
+    const int in_buf = (bounce + 1) & 1;
+    const int cnt = *p.defer_count;
+    if ((p.debug & 16) && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
+    for (int q = blockIdx.x * kBlock + threadIdx.x; q < cnt; q += gridDim.x * kBlock) {
+        const int j = p.defer_slots[q];
+        const int src = slot_source(p, j);
+        const float4 a = p.ray[in_buf][0][src];
+        const float4 b = p.ray[in_buf][1][src];
+        const Hit h = intersect_scene<ACCEL_GRID_FAST, kBlock>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
+                                                               s_stack + threadIdx.x, s_hs + threadIdx.x);
+        p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+        p.hitm[j] = h.model;
     }
 }
 
@@ -932,6 +1375,7 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
+        *p.defer_count = 0;
     }
 }
 
@@ -1063,22 +1507,30 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     {
         // Persistent trace (ACCEL_BVH): hit buffer + work counter; PT_TRACE_SPLIT=0 keeps the fused kernel.
         const char* e = std::getenv("PT_TRACE_SPLIT");
-        split_trace = cfg.accel == ACCEL_BVH && !(e && std::atoi(e) == 0);
+        // default: on for ACCEL_BVH; opt-in (PT_TRACE_SPLIT=1) for ACCEL_GRID_FAST, where the
+        // persistent kernel is still slower than the fused one
+        const int want = e ? std::atoi(e) : (cfg.accel == ACCEL_BVH ? 1 : 0);
+        split_trace = (cfg.accel == ACCEL_BVH || cfg.accel == ACCEL_GRID_FAST) && want != 0;
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
+        const char* tf = std::getenv("PT_TRACE_FLAGS");
+        kp.trace_flags = tf ? std::atoi(tf) : 11;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
-        const int w = wpc ? std::max(1, std::atoi(wpc)) : 20;
+        const int w = wpc ? std::max(1, std::atoi(wpc)) : (cfg.accel == ACCEL_GRID_FAST ? 16 : 20);   // resident waves per CU
         trace_blocks = std::max(1, cus) * w;
         const size_t hcap = split_trace ? cap : 1;
         PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
         PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.trace_next, nullptr, sizeof(int), stream));
+        PT_HIP(upload(allocs, &kp.defer_slots, nullptr, hcap * sizeof(int), stream));
+        PT_HIP(upload(allocs, &kp.defer_count, nullptr, sizeof(int), stream));
+        PT_HIP(hipMemsetAsync(kp.defer_count, 0, sizeof(int), stream));
         PT_HIP(hipMemsetAsync(kp.trace_next, 0, sizeof(int), stream));
     }
-    PT_HIP(upload(allocs, &kp.segments, nullptr, (8 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, (8 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (16 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (16 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -1103,6 +1555,27 @@ int Renderer::launchPrimary() {
     PT_HIP(hipGetLastError());
     cache_valid = true;
     return 0;
+}
+
+void Renderer::launchTrace(int b) {
+    const dim3 g((unsigned)trace_blocks), t(64);
+    if (cfg.accel == ACCEL_GRID_FAST) {
+        if (kp.trace_flags & 8) hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b);
+        else hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, stream, kp, b);
+        return;
+    }
+    switch (kp.trace_flags & 15) {
+        case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, stream, kp, b); break;
+        case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, stream, kp, b); break;
+        case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, stream, kp, b); break;
+        case 3: hipLaunchKernelGGL((k_trace_bvh<64, 3>), g, t, 0, stream, kp, b); break;
+        case 4: hipLaunchKernelGGL((k_trace_bvh<64, 4>), g, t, 0, stream, kp, b); break;
+        case 5: hipLaunchKernelGGL((k_trace_bvh<64, 5>), g, t, 0, stream, kp, b); break;
+        case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, stream, kp, b); break;
+        case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, stream, kp, b); break;
+        case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, stream, kp, b); break;
+        default: hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, stream, kp, b); break;
+    }
 }
 
 template <bool FIRST, int BS>
@@ -1158,7 +1631,11 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
             if (b > 0 && split_trace) {
-                hipLaunchKernelGGL(k_trace_bvh<64>, dim3((unsigned)trace_blocks), dim3(64), 0, stream, kp, b);
+                launchTrace(b);
+                if (cfg.accel == ACCEL_GRID_FAST) {
+                    PT_HIP(hipGetLastError());
+                    hipLaunchKernelGGL(k_trace_deferred, dim3(256), dim3(kBlock), 0, stream, kp, b);
+                }
                 PT_HIP(hipGetLastError());
                 if (profiling) {
                     hipEventRecord(e1, stream);
@@ -1244,11 +1721,11 @@ long long Renderer::segments() {
 
 int Renderer::segmentsPerBounce(long long* out, int n) {
     if (!allocated) { last_error = "not allocated"; return -1; }
-    unsigned long long v[8 + kMaxBounceCounters];
+    unsigned long long v[16 + kMaxBounceCounters];
     PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n && i < kMaxBounceCounters + 7; i++) out[i] = (long long)v[1 + i];
-    for (int i = kMaxBounceCounters + 7; i < n; i++) out[i] = 0;
+    for (int i = 0; i < n && i < kMaxBounceCounters + 15; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters + 15; i < n; i++) out[i] = 0;
     return 0;
 }
 

@@ -26,6 +26,10 @@ KERNELS = {
     "k_bounce<true, 1,": "k_bounce<true,bvh>",
     "k_bounce<true, 0,": "k_bounce<true,grid>",
     "k_scan": "k_scan",
+    "k_trace_bvh<": "k_trace_bvh",
+    "k_trace_gf<": "k_trace_gf",
+    "k_trace_deferred": "k_trace_deferred",
+    "k_bounce<false, 3,": "k_bounce<false,hitbuf>",
 }
 
 

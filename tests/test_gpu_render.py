@@ -237,3 +237,29 @@ def test_grid_fast_hitset_overflow_falls_back_exactly(gpu, pt_mod, oracle_mod, a
     assert_bitexact(mm, om, "model")
     assert_bitexact(t, ot, "dist")
     assert_bitexact(nn[om >= 0], on[om >= 0], "normal")
+
+
+@pytest.mark.parametrize("accel,env", [
+    (1, {"PT_TRACE_SPLIT": "0"}),
+    (1, {"PT_TRACE_FLAGS": "0"}),
+    (1, {"PT_TRACE_FLAGS": "3"}),
+    (1, {"PT_TRACE_FLAGS": "4", "PT_TRACE_REFILL": "1"}),
+    (1, {"PT_TRACE_FLAGS": "11", "PT_TRACE_WAVES_PER_CU": "1"}),
+    (2, {"PT_TRACE_SPLIT": "1", "PT_TRACE_FLAGS": "3"}),
+    (2, {"PT_TRACE_SPLIT": "1", "PT_TRACE_FLAGS": "11", "PT_TRACE_REFILL": "48"}),
+])
+def test_trace_kernel_variants_bitexact(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, env):
+    """Every persistent-trace variant (fused / split, refill policy, phase
+    scheduling, one wave per CU) renders the oracle's image bit for bit."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for path, w, h in ((synthetic.diffuse_scene(synth_dir, ntri=3000, seed=7, metallic=True), 96, 72),
+                       (REF_SCENE, 80, 64)):
+        s = P.Scene(path)
+        s.build(bvh=True)
+        cfg = P.RenderConfig(width=w, height=h, iterations=2, max_bounces=8, accel=accel)
+        img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+        assert seg == oseg
+        assert_bitexact(img, oimg, "image")
