@@ -34,6 +34,12 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP_TRACE
 #define PT_HITCAP_TRACE 4     // hit-set entries per lane in the persistent grid_fast trace (overflow -> deferred)
 #endif
+#ifndef PT_WALK_BURST
+#define PT_WALK_BURST 8       // DDA voxels per persistent-loop iteration (grid_fast trace)
+#endif
+#ifndef PT_TRACE_STATS
+#define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
+#endif
 #ifndef PT_MINWAVES
 #define PT_MINWAVES 5
 #endif
@@ -258,7 +264,7 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
         n_nodes++;
         if (bvh_step<STRIDE>(p, o, d, inv, cur, sp, stack, best, best_tri, any, n_tris)) break;
     }
-    if (p.debug & 8) {
+    if (PT_TRACE_STATS && (p.debug & 8)) {
         atomicAdd(p.segments + 4 + kMaxBounceCounters, (unsigned long long)n_nodes);
         atomicAdd(p.segments + 5 + kMaxBounceCounters, (unsigned long long)n_tris);
         atomicAdd(p.segments + 6 + kMaxBounceCounters, 1ull);
@@ -525,11 +531,11 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     const f3 pt = o + d * t_box;
     if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) return false;
     const f3 ninv = node_inv(inv);
-    if (p.debug & 2) return bvh_closest<STRIDE>(p, M, o, d, ninv, best, best_tri, stack);   // timing-only ablation
+    if (PT_TRACE_STATS && (p.debug & 2)) return bvh_closest<STRIDE>(p, M, o, d, ninv, best, best_tri, stack);   // timing-only ablation
     float tmin;
     int nh = bvh_collect<STRIDE, true>(p, M, o, d, ninv, stack, hs, &tmin);
     if (nh == 0) return false;           // no accepted triangle anywhere on the ray: no hit voxel
-    if ((p.debug & 1) && nh > 0) {       // timing-only ablation: no walk
+    if (PT_TRACE_STATS && (p.debug & 1) && nh > 0) {       // timing-only ablation: no walk
         for (int h = 0; h < nh; h++) {
             const float t = __int_as_float(hs[h * STRIDE].x);
             if (t < best) { best = t; best_tri = hs[h * STRIDE].y; }
@@ -542,7 +548,7 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
         w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
         done = w.final_min || w.tw < tmin + M.reach;
         if (!done) {                                                       // tier 2 in LDS
-            if (p.debug & 4) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);
+            if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);
             nh = bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin);
             if (nh >= 0) {
                 w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
@@ -553,10 +559,10 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     if (!done) {
         // LDS hit set overflowed: the same two tiers in a 64-entry block of the
         // global pool (cold path, kept out of line).
-        if (p.debug & 4) atomicAdd(p.segments + 2 + kMaxBounceCounters, 1ull);
+        if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 2 + kMaxBounceCounters, 1ull);
         done = grid_hitset_pool<STRIDE>(p, M, o, d, inv, ninv, pt, t_box, stack, w);
         if (!done) {
-            if (p.debug & 4) atomicAdd(p.segments + 3 + kMaxBounceCounters, 1ull);
+            if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 3 + kMaxBounceCounters, 1ull);
             return grid_closest(p, M, o, d, inv, best, best_tri);   // exact list-walking DDA
         }
     }
@@ -771,6 +777,8 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
     bool any = false, exhausted = false;
+    unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
+    unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
     int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // wave's claimed source block (uniform)
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
@@ -841,6 +849,12 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
             const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
                       c4 = __popcll(__ballot(state == 4));
             phase = (c2 >= c4 && c2 >= c1) ? 2 : (c4 >= c1 ? 4 : 1);
+        }
+        if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
+            st_iter++;
+            if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
+            if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
+            if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
         }
         if ((phase & 1) && state == 1) {                // advance to the next model that survives culling
             for (;;) {
@@ -961,6 +975,15 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
             state = 1;
         }
     }
+    if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
+        atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
+        atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
+        atomicAdd(p.segments + 12 + kMaxBounceCounters, st_sel);
+        atomicAdd(p.segments + 16 + kMaxBounceCounters, it_node);
+        atomicAdd(p.segments + 17 + kMaxBounceCounters, it_leaf);
+        atomicAdd(p.segments + 19 + kMaxBounceCounters, it_sel);
+    }
 }
 
 // Persistent grid_fast trace for one bounce: computeRayGridIntersection
@@ -997,16 +1020,11 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
     w.tested = 0; w.bt = kFMax; w.hit = false;
     bool exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
+    unsigned long long it_node = 0, it_leaf = 0, it_walk = 0, it_sel = 0;
     for (unsigned iters = 0;; iters++) {
         const unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (p.debug & 16) {
-            st_iter++;
-            st_node += __popcll(__ballot(state == 2));
-            st_leaf += __popcll(__ballot(state == 4));
-            st_walk += __popcll(__ballot(state == 5));
-            st_sel += __popcll(__ballot(state == 1));
-        }
+        if (PT_TRACE_STATS && (p.debug & 16)) st_iter++;
         if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
@@ -1046,9 +1064,15 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
             if (c5 > cm) { phase = 8; cm = c5; }
             if (c1 > cm) { phase = 1; cm = c1; }
         }
+        if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
+            if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
+            if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
+            if (phase & 8) { st_walk += __popcll(__ballot(state == 5)); it_walk++; }
+            if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
+        }
         if ((phase & 1) && state == 1) {
             for (;;) {
-                if (p.debug & 16) atomicAdd(p.segments + 13 + kMaxBounceCounters, 1ull);
+                if (PT_TRACE_STATS && (p.debug & 16)) atomicAdd(p.segments + 13 + kMaxBounceCounters, 1ull);
                 im++;
                 if (im >= p.nmodels) {
                     const Hit h = make_hit(p, gdist, gmodel, gtri);
@@ -1172,7 +1196,10 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
                 state = 5;
             }
         } else if ((phase & 8) && state == 5) {
-            if (walk_step<BS>(p, d, hs, nh, tmin, w)) {
+            // several voxels per iteration: a walk step is cheap next to the loop's own overhead
+            bool ended = false;
+            for (int q = 0; q < PT_WALK_BURST && !ended; q++) ended = walk_step<BS>(p, d, hs, nh, tmin, w);
+            if (ended) {
                 const ModelRec& M = p.models[im];
                 const bool final_min = w.bk >= 0 && w.bt == tmin;
                 const float tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
@@ -1190,12 +1217,16 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
             }
         }
     }
-    if ((p.debug & 16) && lane == 0) {
+    if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
         atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
         atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
         atomicAdd(p.segments + 11 + kMaxBounceCounters, st_walk);
         atomicAdd(p.segments + 12 + kMaxBounceCounters, st_sel);
+        atomicAdd(p.segments + 16 + kMaxBounceCounters, it_node);
+        atomicAdd(p.segments + 17 + kMaxBounceCounters, it_leaf);
+        atomicAdd(p.segments + 18 + kMaxBounceCounters, it_walk);
+        atomicAdd(p.segments + 19 + kMaxBounceCounters, it_sel);
     }
 }
 
@@ -1206,7 +1237,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_deferred(KParams p, int bounce
     __shared__ int4 s_hs[kHitCap * kBlock];
     const int in_buf = (bounce + 1) & 1;
     const int cnt = *p.defer_count;
-    if ((p.debug & 16) && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
+    if ((PT_TRACE_STATS && (p.debug & 16)) && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
     for (int q = blockIdx.x * kBlock + threadIdx.x; q < cnt; q += gridDim.x * kBlock) {
         const int j = p.defer_slots[q];
         const int src = slot_source(p, j);
@@ -1529,8 +1560,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         PT_HIP(hipMemsetAsync(kp.defer_count, 0, sizeof(int), stream));
         PT_HIP(hipMemsetAsync(kp.trace_next, 0, sizeof(int), stream));
     }
-    PT_HIP(upload(allocs, &kp.segments, nullptr, (16 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, (16 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (32 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (32 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -1721,11 +1752,11 @@ long long Renderer::segments() {
 
 int Renderer::segmentsPerBounce(long long* out, int n) {
     if (!allocated) { last_error = "not allocated"; return -1; }
-    unsigned long long v[16 + kMaxBounceCounters];
+    unsigned long long v[32 + kMaxBounceCounters];
     PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n && i < kMaxBounceCounters + 15; i++) out[i] = (long long)v[1 + i];
-    for (int i = kMaxBounceCounters + 15; i < n; i++) out[i] = 0;
+    for (int i = 0; i < n && i < kMaxBounceCounters + 31; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters + 31; i < n; i++) out[i] = 0;
     return 0;
 }
 

@@ -70,12 +70,14 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
-        allc = rs[v].segments_per_bounce(78)
+        allc = rs[v].segments_per_bounce(94)
         if allc[71]:
             it = allc[71]
             out[v]["trace_iters_per_wave_total"] = it
-            out[v]["lanes_per_iter"] = {k: round(allc[i] / it, 2) for k, i in
-                                        (("node", 72), ("leaf", 73), ("walk", 74), ("select", 75))}
+            ph = {k: (allc[i + 7], allc[i]) for k, i in
+                  (("node", 72), ("leaf", 73), ("walk", 74), ("select", 75))}
+            out[v]["phase_iters"] = {k: a for k, (a, b) in ph.items()}
+            out[v]["lanes_per_phase_iter"] = {k: round(b / max(a, 1), 2) for k, (a, b) in ph.items()}
             out[v]["select_loop_trips"] = allc[76]
             out[v]["deferred"] = allc[77]
         diag = allc[64:67]
