@@ -42,6 +42,9 @@ struct KParams {
     const BvhNode* bvh;
     const int* bvh_tri;
     const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
+    const Bvh4Node* bvh4;       // 4-wide BLAS (persistent traces)
+    int* spill;                 // traversal-stack spill beyond the LDS entries, lane-minor
+    int spill_stride;           // lanes in the spill layout
     // frame
     int width, height, npix, max_bounces, nblocks, chunk;
     float step_x, step_y, cam_x, cam_y, cam_z, plane_z;

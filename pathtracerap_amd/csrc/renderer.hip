@@ -285,7 +285,7 @@ __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 i
                            int4* __restrict__ hs, float* tmin_out) {
     int nh = 0;
     float tmin = kFMax;
-    const float margin = 2.0f * M.reach;
+    const float margin = M.wdelta + M.reach;
     int sp = 0;
     int cur = M.bvh_root;
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
@@ -366,7 +366,7 @@ struct WalkResult {
     float t;         // winning member's t (valid when has_best)
     int tri;
     bool has_best;
-    bool final_min;  // a member with t == tmin was tested: the result is final
+    bool final_min;  // a member with t == tmin was tested in a voxel entered before tmin + wdelta: final
     float tw;        // ray parameter (from the model-space origin) where the walk stopped
 };
 
@@ -387,6 +387,8 @@ struct Walk {
     float bt;
     int bk, bi;
     bool hit;
+    float te;                      // entry parameter (from pt) of the current voxel
+    float tbe;                     // entry parameter of the voxel where the current best was tested
 };
 
 __device__ __forceinline__ void walk_init(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, Walk& w) {
@@ -413,6 +415,8 @@ __device__ __forceinline__ void walk_init(const KParams& p, const ModelRec& M, f
     w.bk = -1;
     w.bi = -1;
     w.hit = false;
+    w.te = 0.0f;
+    w.tbe = 0.0f;
 }
 
 template <int HSTRIDE>
@@ -443,7 +447,9 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
                 if (!((w.tested >> h) & 1ull)) {
                     w.tested |= 1ull << h;
                     const float t = __int_as_float(e.x);
-                    if (t < w.bt || (t == w.bt && (k < w.bk || (k == w.bk && e.y < w.bi)))) { w.bt = t; w.bk = k; w.bi = e.y; }
+                    if (t < w.bt || (t == w.bt && (k < w.bk || (k == w.bk && e.y < w.bi)))) {
+                        w.bt = t; w.bk = k; w.bi = e.y; w.tbe = w.te;
+                    }
                 }
             }
         }
@@ -464,14 +470,17 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
     if (w.tmax.x < w.tmax.y && w.tmax.x < w.tmax.z) {
         w.ix = ix + sx;
         if (w.ix == (d.x > 0.0f ? p.gdim[0] : -1) || w.tmax.x >= kFMax) return true;
+        w.te = w.tmax.x;
         w.tmax.x += w.delta.x;
     } else if (w.tmax.y < w.tmax.z) {
         w.iy = iy + sy;
         if (w.iy == (d.y > 0.0f ? p.gdim[1] : -1) || w.tmax.y >= kFMax) return true;
+        w.te = w.tmax.y;
         w.tmax.y += w.delta.y;
     } else {
         w.iz = iz + sz;
         if (w.iz == (d.z > 0.0f ? p.gdim[2] : -1) || w.tmax.z >= kFMax) return true;
+        w.te = w.tmax.z;
         w.tmax.z += w.delta.z;
     }
     return false;
@@ -489,7 +498,7 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
     r.t = w.bt;
     r.tri = w.bi;
     r.has_best = w.bk >= 0;
-    r.final_min = w.bk >= 0 && w.bt == tmin;
+    r.final_min = w.bk >= 0 && w.bt == tmin && t_box + w.tbe < tmin + M.wdelta;
     r.tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
     return r;
 }
@@ -508,7 +517,7 @@ __device__ bool grid_hitset_pool(const KParams& p, const ModelRec& M, f3 o, f3 d
     int ng = bvh_collect<STRIDE, true, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin);
     if (ng < 0) return false;
     w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin);
-    if (w.final_min || w.tw < tmin + M.reach) return true;
+    if (w.final_min || w.tw < tmin + M.wdelta) return true;
     ng = bvh_collect<STRIDE, false, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin);
     if (ng < 0) return false;
     w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin);
@@ -517,12 +526,12 @@ __device__ bool grid_hitset_pool(const KParams& p, const ModelRec& M, f3 o, f3 d
 
 // computeRayGridIntersection (Renderer.cpp:238-360), result-identical, via the
 // BLAS hit set and hitset_walk.
-// Tier 1 collects members with t <= t_min + 2R only (R = ModelRec::reach: a
-// member whose voxel box the walk enters at parameter tau has t <= tau + R).
-// It is exact when the walk tests a minimum-t member (every box entered before
-// that belongs to a member with t <= t_min + 2R) or stops before parameter
-// t_min + R (no uncollected member's box is reachable).  Otherwise tier 2
-// collects the whole set; on hit-set overflow the list-walking DDA runs.
+// Tier 1 collects members with t <= t_min + W + R only (R = ModelRec::reach: a
+// member whose voxel box the walk enters at parameter tau has t <= tau + R;
+// W = ModelRec::wdelta), so the simulated walk equals the reference walk up to
+// parameter X = t_min + W.  It is exact when the walk tests a minimum-t member
+// in a voxel entered before X, or stops before X.  Otherwise tier 2 collects
+// the whole set; on hit-set overflow the global pool, then the list-walking DDA.
 template <int STRIDE>
 __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, float& best, int& best_tri,
                             int* __restrict__ stack, int4* __restrict__ hs) {
@@ -546,7 +555,7 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     bool done = false;
     if (nh > 0) {
         w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
-        done = w.final_min || w.tw < tmin + M.reach;
+        done = w.final_min || w.tw < tmin + M.wdelta;
         if (!done) {                                                       // tier 2 in LDS
             if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);
             nh = bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin);
@@ -740,6 +749,59 @@ __device__ __forceinline__ int slot_source(const KParams& p, int j) {
 // survivors sit at [b*chunk, b*chunk + cnt_b) and own dense slots
 // [blk_off[b], blk_off[b] + cnt_b), so no slot->source search is needed.
 // Every wave exits once all blocks are claimed and its lanes are idle.
+// Per-lane traversal stack: kStack entries in LDS (lane-contiguous), deeper
+// entries in a global spill area laid out lane-minor (p.spill_stride lanes).
+template <int BS>
+__device__ __forceinline__ void spush_t(int* stack, int* spill, int stride, int sp, int e) {
+    if (sp < kStack) stack[sp * BS] = e;
+    else spill[(size_t)(sp - kStack) * stride] = e;
+}
+template <int BS>
+__device__ __forceinline__ int spop_t(const int* stack, const int* spill, int stride, int sp) {
+    return sp < kStack ? stack[sp * BS] : spill[(size_t)(sp - kStack) * stride];
+}
+#define spush(stack, spill, sp, e) spush_t<BS>(stack, spill, p.spill_stride, sp, e)
+#define spop(stack, spill, sp) spop_t<BS>(stack, spill, p.spill_stride, sp)
+
+// Visit a 4-wide node: slab-test the four children against (o, inv) with the
+// closest-hit bound `best`; returns the number of hit children and their stack
+// entries nearest first (node: idx << 1; leaf: first << 4 | count << 1 | 1).
+__device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 inv, float bound,
+                                          int& e0, int& e1, int& e2, int& e3) {
+    const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
+    const float4 lx = n4[0], hx = n4[1], ly = n4[2], hy = n4[3], lz = n4[4], hz = n4[5];
+    const int4 lk = *reinterpret_cast<const int4*>(n4 + 6);
+    const int4 ct = *reinterpret_cast<const int4*>(n4 + 7);
+    float k[4];
+    int e[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float lox = c == 0 ? lx.x : c == 1 ? lx.y : c == 2 ? lx.z : lx.w;
+        const float hix = c == 0 ? hx.x : c == 1 ? hx.y : c == 2 ? hx.z : hx.w;
+        const float loy = c == 0 ? ly.x : c == 1 ? ly.y : c == 2 ? ly.z : ly.w;
+        const float hiy = c == 0 ? hy.x : c == 1 ? hy.y : c == 2 ? hy.z : hy.w;
+        const float loz = c == 0 ? lz.x : c == 1 ? lz.y : c == 2 ? lz.z : lz.w;
+        const float hiz = c == 0 ? hz.x : c == 1 ? hz.y : c == 2 ? hz.z : hz.w;
+        const int link = c == 0 ? lk.x : c == 1 ? lk.y : c == 2 ? lk.z : lk.w;
+        const int cnt = c == 0 ? ct.x : c == 1 ? ct.y : c == 2 ? ct.z : ct.w;
+        const float lo[3] = {lox, loy, loz}, hi[3] = {hix, hiy, hiz};
+        float tn, tf;
+        node_slab(lo, hi, o, inv, tn, tf);
+        const bool h = cnt >= 0 && tn <= tf && tf >= -kEps && tn <= bound;
+        k[c] = h ? tn : __int_as_float(0x7f800000);
+        e[c] = cnt == 0 ? (link << 1) : ((link << 4) | (cnt << 1) | 1);
+    }
+    // sort (key, entry) ascending: 5 compare-exchanges
+#define PT_CX(a, b) { const bool sw = k[b] < k[a]; const float tk = sw ? k[b] : k[a]; k[b] = sw ? k[a] : k[b]; k[a] = tk; \
+                      const int te = sw ? e[b] : e[a]; e[b] = sw ? e[a] : e[b]; e[a] = te; }
+    PT_CX(0, 1) PT_CX(2, 3) PT_CX(0, 2) PT_CX(1, 3) PT_CX(1, 2)
+#undef PT_CX
+    const float inf = __int_as_float(0x7f800000);
+    const int n = (k[0] != inf) + (k[1] != inf) + (k[2] != inf) + (k[3] != inf);
+    e0 = e[0]; e1 = e[1]; e2 = e[2]; e3 = e[3];
+    return n;
+}
+
 constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
 
 // F (compile-time variant): 1 = model records in LDS, 2 = leaf triangles as
@@ -749,6 +811,7 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     __shared__ int s_stack[kStack * BS];
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
+    int* spill = p.spill + (size_t)blockIdx.x * BS + threadIdx.x;   // stack entries beyond the LDS part
     const bool lds_models = (F & 1) && p.nmodels <= kLdsModels;
     if (lds_models) {
         const int* src = reinterpret_cast<const int*>(p.models);
@@ -776,6 +839,8 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0;    // pending leaves: [lf_i, lf_e) then [lf2_i, lf2_e)
     int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
+    float t2 = kFMax, mreach = 0.0f;                 // grid semantics (F & 32): runner-up t, model reach
+    int vlo1 = 0, vhi1 = 0;                         // and the winner's packed voxel box
     bool any = false, exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
     unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
@@ -874,11 +939,20 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                     break;
                 }
                 const ModelRec& M = models[im];
-                if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (model_culled<(F & 32) ? ACCEL_GRID_FAST : ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
-                ninv = node_inv(mk3(1 / d.x, 1 / d.y, 1 / d.z));
-                cur = M.bvh_root;
+                const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+                if (F & 32) {                           // the grid walk's entry conditions (grid_hitset)
+                    float t_box;
+                    if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
+                    const f3 pt = o + d * t_box;
+                    if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
+                    mreach = M.reach;
+                    t2 = kFMax;
+                }
+                ninv = node_inv(inv);
+                cur = (F & 16) ? M.bvh4_root : M.bvh_root;
                 sp = 0;
                 best = kFMax;
                 best_tri = -1;
@@ -894,10 +968,30 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
             float t;
             if (tri_test_rec(A, B, C, o, d, t)) {
                 any = true;
-                if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+                if (F & 32) {                           // keep the runner-up t and the winner's voxel box
+                    if (t < best || (t == best && it < best_tri)) {
+                        t2 = fminf(t2, best); best = t; best_tri = it;
+                        vlo1 = __float_as_int(B.w); vhi1 = __float_as_int(C.w);
+                    } else if (t < t2) {
+                        t2 = t;
+                    }
+                    if (t != t) t2 = __int_as_float(0xff800000);   // NaN member: force the full walk
+
+                } else if (t < best || (t == best && it < best_tri)) {
+                    best = t; best_tri = it;
+                }
             }
             lf_i++;
-            if (lf_i == lf_e) {
+            if ((F & 16) && lf_i == lf_e) {             // 4-wide: everything pending is on the stack
+                if (sp == 0) {
+                    model_done = true;
+                } else {
+                    sp--;
+                    const int e = spop(stack, spill, sp);
+                    if (e & 1) { lf_i = e >> 4; lf_e = lf_i + ((e >> 1) & 7); }
+                    else { cur = e >> 1; state = 2; }
+                }
+            } else if (lf_i == lf_e) {
                 if (lf2_i < lf2_e) {                    // second leaf child
                     lf_i = lf2_i; lf_e = lf2_e;
                     lf2_i = lf2_e = 0;
@@ -913,7 +1007,28 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                 }
             }
         } else if ((phase & 2) && state == 2) {
-            if (!leaf_state) {
+            if (F & 16) {
+                // 4-wide node: four slab tests, nearest hit child next, the
+                // others pushed far-to-near (leaves as tagged entries)
+                int e0, e1, e2, e3;
+                const int nhit = bvh4_visit(p, cur, o, ninv, (F & 32) ? best + mreach : best, e0, e1, e2, e3);
+                if (nhit == 0) {
+                    if (sp == 0) {
+                        model_done = true;
+                    } else {
+                        sp--;
+                        e0 = spop(stack, spill, sp);
+                    }
+                } else {
+                    if (nhit > 3) { spush(stack, spill, sp, e3); sp++; }
+                    if (nhit > 2) { spush(stack, spill, sp, e2); sp++; }
+                    if (nhit > 1) { spush(stack, spill, sp, e1); sp++; }
+                }
+                if (!model_done) {
+                    if (e0 & 1) { lf_i = e0 >> 4; lf_e = lf_i + ((e0 >> 1) & 7); state = 4; }
+                    else cur = e0 >> 1;
+                }
+            } else if (!leaf_state) {
                 model_done = bvh_step<BS>(p, o, d, ninv, cur, sp, stack, best, best_tri, any, n_tris);
             } else {
                 // node visit; hit leaf children become pending leaves (tested one
@@ -930,8 +1045,9 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                 float tn0, tf0, tn1, tf1;
                 node_slab(lo0, hi0, o, ninv, tn0, tf0);
                 node_slab(lo1, hi1, o, ninv, tn1, tf1);
-                const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
-                const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
+                const float bnd = (F & 32) ? best + mreach : best;
+                const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bnd;
+                const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bnd;
                 const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
                 const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
                 // next node after the leaves: same rule as bvh_step
@@ -968,11 +1084,31 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
             }
         }
         if (model_done) {
-            if (any) {
+            state = 1;
+            if ((F & 32) && any) {
+                // Grid semantics without the walk: the reference's result for this model is
+                // the closest member when no other member lies within `reach` of it and its
+                // hit point is safely inside its own voxel box; else the full
+                // grid_hitset tiers run for this ray in k_trace_deferred.
+                const ModelRec& M = models[im];
+                bool ok = t2 > best + mreach;
+                const f3 ps = o + d * best;
+                const float fx = (ps.x - M.bbox[0] + kEps) / M.vw[0];
+                const float fy = (ps.y - M.bbox[1] + kEps) / M.vw[1];
+                const float fz = (ps.z - M.bbox[2] + kEps) / M.vw[2];
+                constexpr float m = 1e-3f;
+                ok = ok && fx >= (float)(vlo1 & 1023) + m && fx <= (float)((vhi1 & 1023) + 1) - m;
+                ok = ok && fy >= (float)((vlo1 >> 10) & 1023) + m && fy <= (float)(((vhi1 >> 10) & 1023) + 1) - m;
+                ok = ok && fz >= (float)((vlo1 >> 20) & 1023) + m && fz <= (float)(((vhi1 >> 20) & 1023) + 1) - m;
+                if (!ok) {
+                    p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                    state = 0;
+                }
+            }
+            if (state == 1 && any) {
                 const float dd = model_hit_dist(models[im], o, d, best, ow);
                 if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
             }
-            state = 1;
         }
     }
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
@@ -1090,7 +1226,7 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
                 const f3 pt = o + d * t_box;
                 if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
                 ninv = node_inv(inv);
-                margin = 2.0f * M.reach;
+                margin = M.wdelta + M.reach;
                 cur = M.bvh_root;
                 sp = 0;
                 nh = 0;
@@ -1201,9 +1337,9 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
             for (int q = 0; q < PT_WALK_BURST && !ended; q++) ended = walk_step<BS>(p, d, hs, nh, tmin, w);
             if (ended) {
                 const ModelRec& M = p.models[im];
-                const bool final_min = w.bk >= 0 && w.bt == tmin;
+                const bool final_min = w.bk >= 0 && w.bt == tmin && t_box + w.tbe < tmin + M.wdelta;
                 const float tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
-                if (final_min || tw < tmin + M.reach) {
+                if (final_min || tw < tmin + M.wdelta) {
                     if (w.hit) {
                         const float best = w.bk >= 0 ? w.bt : kFMax;
                         const float dd = model_hit_dist(M, o, d, best, ow);
@@ -1232,19 +1368,20 @@ __global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
 
 // Rays k_trace_gf deferred: the full grid_hitset tiers (LDS, global pool,
 // list-walking DDA), one lane per ray.
-__global__ __launch_bounds__(kBlock) void k_trace_deferred(KParams p, int bounce) {
-    __shared__ int s_stack[kStack * kBlock];
-    __shared__ int4 s_hs[kHitCap * kBlock];
+template <int BS>
+__global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
+    __shared__ int s_stack[kStack * BS];
+    __shared__ int4 s_hs[kHitCap * BS];
     const int in_buf = (bounce + 1) & 1;
     const int cnt = *p.defer_count;
     if ((PT_TRACE_STATS && (p.debug & 16)) && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
-    for (int q = blockIdx.x * kBlock + threadIdx.x; q < cnt; q += gridDim.x * kBlock) {
+    for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
         const int j = p.defer_slots[q];
         const int src = slot_source(p, j);
         const float4 a = p.ray[in_buf][0][src];
         const float4 b = p.ray[in_buf][1][src];
-        const Hit h = intersect_scene<ACCEL_GRID_FAST, kBlock>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
-                                                               s_stack + threadIdx.x, s_hs + threadIdx.x);
+        const Hit h = intersect_scene<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
+                                                           s_stack + threadIdx.x, s_hs + threadIdx.x);
         p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
         p.hitm[j] = h.model;
     }
@@ -1502,6 +1639,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
+    PT_HIP(upload(allocs, &kp.bvh4, scene.bvh4_nodes.data(), scene.bvh4_nodes.size() * sizeof(Bvh4Node), stream));
 
     kp.width = cfg.width;
     kp.height = cfg.height;
@@ -1552,6 +1690,14 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const int w = wpc ? std::max(1, std::atoi(wpc)) : (cfg.accel == ACCEL_GRID_FAST ? 16 : 20);   // resident waves per CU
         trace_blocks = std::max(1, cus) * w;
         const size_t hcap = split_trace ? cap : 1;
+        // 4-wide traversal pushes up to 3 entries per level: LDS holds kStack, the rest spills
+        constexpr int kSpillEntries = 64;
+        if (split_trace && (kp.trace_flags & 16) && 3 * scene.bvh4_max_depth > kStack + kSpillEntries) {
+            last_error = "BVH4 too deep for the traversal stack";
+            return -1;
+        }
+        kp.spill_stride = split_trace && (kp.trace_flags & 16) ? trace_blocks * 64 : 1;
+        PT_HIP(upload(allocs, &kp.spill, nullptr, (size_t)kp.spill_stride * kSpillEntries * sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
         PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.trace_next, nullptr, sizeof(int), stream));
@@ -1591,11 +1737,12 @@ int Renderer::launchPrimary() {
 void Renderer::launchTrace(int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
-        if (kp.trace_flags & 8) hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b);
+        if (kp.trace_flags & 32) hipLaunchKernelGGL((k_trace_bvh<64, 43>), g, t, 0, stream, kp, b);
+        else if (kp.trace_flags & 8) hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b);
         else hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, stream, kp, b);
         return;
     }
-    switch (kp.trace_flags & 15) {
+    switch (kp.trace_flags & 31) {
         case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, stream, kp, b); break;
         case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, stream, kp, b); break;
         case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, stream, kp, b); break;
@@ -1605,6 +1752,8 @@ void Renderer::launchTrace(int b) {
         case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, stream, kp, b); break;
         case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, stream, kp, b); break;
         case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, stream, kp, b); break;
+        case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, stream, kp, b); break;
+        case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, stream, kp, b); break;
         default: hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, stream, kp, b); break;
     }
 }
@@ -1665,7 +1814,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
                 launchTrace(b);
                 if (cfg.accel == ACCEL_GRID_FAST) {
                     PT_HIP(hipGetLastError());
-                    hipLaunchKernelGGL(k_trace_deferred, dim3(256), dim3(kBlock), 0, stream, kp, b);
+                    hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)trace_blocks), dim3(64), 0, stream, kp, b);
                 }
                 PT_HIP(hipGetLastError());
                 if (profiling) {

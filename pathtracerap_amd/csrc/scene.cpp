@@ -602,21 +602,36 @@ void Scene::buildDeviceTables() {
         r.tri_start = mesh.triangle_indices.start_index;
         r.tri_end = mesh.triangle_indices.end_index;
         r.bvh_root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m.mesh_index];
+        r.bvh4_root = mesh_bvh4_root.empty() ? -1 : mesh_bvh4_root[m.mesh_index];
         for (int k = 0; k < 3; k++) r.color[k] = m.mat.color[k];
         world_box(m, mesh, r.bvh_root, r.wbox);
-        // Bounded hit-set collection (ACCEL_GRID_FAST): a triangle whose voxel box the
-        // DDA enters at ray parameter tau has its hit within tau + R.
-        double tmax_diag = 0;
+        // Bounded hit-set collection (ACCEL_GRID_FAST).  A member h whose voxel box the
+        // DDA enters at ray parameter tau has its hit within tau + R_h, R_h = the diameter
+        // of its voxel box grown by the test's tolerance region (<= 1% of the triangle's
+        // bbox diagonal outside the bbox on each side) and the DDA's +EPSILON index shift.
+        // reach = max_h R_h (+2% and a rounding slack); wdelta = the tier-1 window.
+        double rmax = 0;
         for (int t = mesh.triangle_indices.start_index; t < mesh.triangle_indices.end_index; t++) {
             BoundingBox tb;
             for (int j = 0; j < 3; j++) tb.update(vertices[triangles[t].vertex_indices[j]].position);
             const double dx = (double)tb.max.x - tb.min.x, dy = (double)tb.max.y - tb.min.y, dz = (double)tb.max.z - tb.min.z;
-            tmax_diag = std::max(tmax_diag, std::sqrt(dx * dx + dy * dy + dz * dz));
+            const double tdiag = std::sqrt(dx * dx + dy * dy + dz * dz);
+            const int lo = tri_vbox[2 * (size_t)t], hi = tri_vbox[2 * (size_t)t + 1];
+            double vb = 0;
+            for (int k = 0; k < 3; k++) {
+                const double n = (double)(((hi >> (10 * k)) & 1023) - ((lo >> (10 * k)) & 1023) + 1);
+                vb += (n * g.voxel_width[k]) * (n * g.voxel_width[k]);
+            }
+            rmax = std::max(rmax, std::sqrt(vb) + 0.02 * tdiag + 4.0 * (double)kEps);
         }
         const double vd = std::sqrt((double)g.voxel_width[0] * g.voxel_width[0] + (double)g.voxel_width[1] * g.voxel_width[1] +
                                     (double)g.voxel_width[2] * g.voxel_width[2]);
-        const double R = 1.02 * (1.02 * tmax_diag + 3.0 * vd) + 1.0;
+        const double bd = vd * std::sqrt((double)grid_dim[0] * grid_dim[0] + (double)grid_dim[1] * grid_dim[1] +
+                                         (double)grid_dim[2] * grid_dim[2]) / std::sqrt(3.0);
+        const double R = 1.02 * rmax + 1e-4 * bd + 1e-3;
         r.reach = std::isfinite(R) ? (float)R : 3e38f;
+        const double W = 0.05 * vd + 1e-4 * bd + 1e-3;
+        r.wdelta = std::isfinite(W) ? (float)W : 3e38f;
     }
 }
 
@@ -683,8 +698,11 @@ int Scene::build(const int gd[3], bool with_bvh) {
     bvh_nodes.clear();
     bvh_tri_order.clear();
     mesh_bvh_root.assign(meshes.size(), -1);
+    bvh4_nodes.clear();
+    mesh_bvh4_root.assign(meshes.size(), -1);
+    bvh4_max_depth = 0;
     if (with_bvh)
-        for (size_t m = 0; m < meshes.size(); m++) buildBvh((int)m);
+        for (size_t m = 0; m < meshes.size(); m++) { buildBvh((int)m); buildBvh4((int)m); }
     buildDeviceTables();
     built = true;
     return 0;
