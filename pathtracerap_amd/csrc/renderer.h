@@ -66,8 +66,6 @@ struct KParams {
     int* hitm;                          // per-slot model
     int* trace_next;                    // persistent trace: next unclaimed source block, reset by k_scan
     int trace_refill;                   // refill a wave's idle lanes once this many are idle
-    int* defer_slots;                   // grid_fast: slots k_trace_gf handed to k_trace_deferred
-    int* defer_count;                   // reset by k_scan
     int trace_flags;                    // k_trace_bvh variant: 1 LDS model records, 2 leaf steps, 4 block claims
 };
 

@@ -31,12 +31,6 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP
 #define PT_HITCAP 6
 #endif
-#ifndef PT_HITCAP_TRACE
-#define PT_HITCAP_TRACE 4     // hit-set entries per lane in the persistent grid_fast trace (overflow -> deferred)
-#endif
-#ifndef PT_WALK_BURST
-#define PT_WALK_BURST 8       // DDA voxels per persistent-loop iteration (grid_fast trace)
-#endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
 #endif
@@ -282,10 +276,9 @@ constexpr int kHitCapPool = 64;      // global pool block (members); overflow ->
 // Returns the count (-1 on overflow); *tmin_out = smallest t accepted.
 template <int STRIDE, bool BOUNDED, int HSTRIDE = STRIDE, int CAP = kHitCap>
 __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, int* __restrict__ stack,
-                           int4* __restrict__ hs, float* tmin_out) {
+                           int4* __restrict__ hs, float* tmin_out, float margin) {
     int nh = 0;
     float tmin = kFMax;
-    const float margin = M.wdelta + M.reach;
     int sp = 0;
     int cur = M.bvh_root;
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
@@ -488,7 +481,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
 
 template <int HSTRIDE>
 __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
-                                  const int4* __restrict__ hs, int nh, float tmin) {
+                                  const int4* __restrict__ hs, int nh, float tmin, float win) {
     Walk w;
     walk_init(p, M, d, inv, pt, w);
     walk_union<HSTRIDE>(hs, nh, w);
@@ -498,7 +491,7 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
     r.t = w.bt;
     r.tri = w.bi;
     r.has_best = w.bk >= 0;
-    r.final_min = w.bk >= 0 && w.bt == tmin && t_box + w.tbe < tmin + M.wdelta;
+    r.final_min = w.bk >= 0 && w.bt == tmin && t_box + w.tbe < tmin + win;
     r.tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
     return r;
 }
@@ -509,19 +502,21 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
 // block overflows too (the caller then runs the list-walking DDA).
 template <int STRIDE>
 __device__ bool grid_hitset_pool(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, f3 ninv,
-                                              f3 pt, float t_box, int* __restrict__ stack, WalkResult& w) {
+                                 f3 pt, float t_box, int* __restrict__ stack, WalkResult& w) {
     const int blk = atomicAdd(p.hs_pool_next, 1);
     if (blk >= p.hs_pool_blocks) return false;
     int4* g = p.hs_pool + (size_t)blk * kHitCapPool;
-    float tmin;
-    int ng = bvh_collect<STRIDE, true, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin);
-    if (ng < 0) return false;
-    w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin);
-    if (w.final_min || w.tw < tmin + M.wdelta) return true;
-    ng = bvh_collect<STRIDE, false, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin);
-    if (ng < 0) return false;
-    w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin);
-    return true;
+#pragma unroll 1
+    for (int tier = 0; tier < 3; tier++) {
+        const float win = tier == 0 ? M.wdelta : (tier == 1 ? 2.0f * M.reach : 3.0e38f);
+        float tmin;
+        const int ng = tier < 2 ? bvh_collect<STRIDE, true, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin, win + M.reach)
+                                : bvh_collect<STRIDE, false, 1, kHitCapPool>(p, M, o, d, ninv, stack, g, &tmin, 3.0e38f);
+        if (ng < 0) return false;
+        w = hitset_walk<1>(p, M, d, inv, pt, t_box, g, ng, tmin, win);
+        if (tier == 2 || w.final_min || w.tw < tmin + win) return true;
+    }
+    return false;
 }
 
 // computeRayGridIntersection (Renderer.cpp:238-360), result-identical, via the
@@ -541,33 +536,31 @@ __device__ bool grid_hitset(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) return false;
     const f3 ninv = node_inv(inv);
     if (PT_TRACE_STATS && (p.debug & 2)) return bvh_closest<STRIDE>(p, M, o, d, ninv, best, best_tri, stack);   // timing-only ablation
-    float tmin;
-    int nh = bvh_collect<STRIDE, true>(p, M, o, d, ninv, stack, hs, &tmin);
-    if (nh == 0) return false;           // no accepted triangle anywhere on the ray: no hit voxel
-    if (PT_TRACE_STATS && (p.debug & 1) && nh > 0) {       // timing-only ablation: no walk
-        for (int h = 0; h < nh; h++) {
-            const float t = __int_as_float(hs[h * STRIDE].x);
-            if (t < best) { best = t; best_tri = hs[h * STRIDE].y; }
-        }
-        return true;
-    }
+    // Tiers: window W (ModelRec::wdelta), then 2R, then unbounded; each collects
+    // the members a walk exact up to t_min + window needs (margin window + R).
     WalkResult w;
     bool done = false;
-    if (nh > 0) {
-        w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
-        done = w.final_min || w.tw < tmin + M.wdelta;
-        if (!done) {                                                       // tier 2 in LDS
-            if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);
-            nh = bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin);
-            if (nh >= 0) {
-                w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin);
-                done = true;
+#pragma unroll 1
+    for (int tier = 0; tier < 3; tier++) {
+        const float win = tier == 0 ? M.wdelta : (tier == 1 ? 2.0f * M.reach : 3.0e38f);
+        float tmin;
+        const int nh = tier < 2 ? bvh_collect<STRIDE, true>(p, M, o, d, ninv, stack, hs, &tmin, win + M.reach)
+                                : bvh_collect<STRIDE, false>(p, M, o, d, ninv, stack, hs, &tmin, 3.0e38f);
+        if (nh == 0) return false;       // no accepted triangle anywhere on the ray: no hit voxel
+        if (nh < 0) break;               // LDS hit set overflowed
+        if (PT_TRACE_STATS && (p.debug & 1)) {   // timing-only ablation: no walk
+            for (int h = 0; h < nh; h++) {
+                const float t = __int_as_float(hs[h * STRIDE].x);
+                if (t < best) { best = t; best_tri = hs[h * STRIDE].y; }
             }
+            return true;
         }
+        w = hitset_walk<STRIDE>(p, M, d, inv, pt, t_box, hs, nh, tmin, win);
+        if (tier == 2 || w.final_min || w.tw < tmin + win) { done = true; break; }
+        if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 1 + kMaxBounceCounters, 1ull);
     }
     if (!done) {
-        // LDS hit set overflowed: the same two tiers in a 64-entry block of the
-        // global pool (cold path, kept out of line).
+        // LDS hit set overflowed: the same tiers in a 64-entry block of the global pool.
         if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 2 + kMaxBounceCounters, 1ull);
         done = grid_hitset_pool<STRIDE>(p, M, o, d, inv, ninv, pt, t_box, stack, w);
         if (!done) {
@@ -839,8 +832,6 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0;    // pending leaves: [lf_i, lf_e) then [lf2_i, lf2_e)
     int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
-    float t2 = kFMax, mreach = 0.0f;                 // grid semantics (F & 32): runner-up t, model reach
-    int vlo1 = 0, vhi1 = 0;                         // and the winner's packed voxel box
     bool any = false, exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
     unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
@@ -939,18 +930,10 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                     break;
                 }
                 const ModelRec& M = models[im];
-                if (model_culled<(F & 32) ? ACCEL_GRID_FAST : ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
-                if (F & 32) {                           // the grid walk's entry conditions (grid_hitset)
-                    float t_box;
-                    if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
-                    const f3 pt = o + d * t_box;
-                    if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
-                    mreach = M.reach;
-                    t2 = kFMax;
-                }
                 ninv = node_inv(inv);
                 cur = (F & 16) ? M.bvh4_root : M.bvh_root;
                 sp = 0;
@@ -968,18 +951,7 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
             float t;
             if (tri_test_rec(A, B, C, o, d, t)) {
                 any = true;
-                if (F & 32) {                           // keep the runner-up t and the winner's voxel box
-                    if (t < best || (t == best && it < best_tri)) {
-                        t2 = fminf(t2, best); best = t; best_tri = it;
-                        vlo1 = __float_as_int(B.w); vhi1 = __float_as_int(C.w);
-                    } else if (t < t2) {
-                        t2 = t;
-                    }
-                    if (t != t) t2 = __int_as_float(0xff800000);   // NaN member: force the full walk
-
-                } else if (t < best || (t == best && it < best_tri)) {
-                    best = t; best_tri = it;
-                }
+                if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
             }
             lf_i++;
             if ((F & 16) && lf_i == lf_e) {             // 4-wide: everything pending is on the stack
@@ -1011,7 +983,7 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                 // 4-wide node: four slab tests, nearest hit child next, the
                 // others pushed far-to-near (leaves as tagged entries)
                 int e0, e1, e2, e3;
-                const int nhit = bvh4_visit(p, cur, o, ninv, (F & 32) ? best + mreach : best, e0, e1, e2, e3);
+                const int nhit = bvh4_visit(p, cur, o, ninv, best, e0, e1, e2, e3);
                 if (nhit == 0) {
                     if (sp == 0) {
                         model_done = true;
@@ -1045,9 +1017,8 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
                 float tn0, tf0, tn1, tf1;
                 node_slab(lo0, hi0, o, ninv, tn0, tf0);
                 node_slab(lo1, hi1, o, ninv, tn1, tf1);
-                const float bnd = (F & 32) ? best + mreach : best;
-                const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bnd;
-                const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bnd;
+                const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
+                const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
                 const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
                 const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
                 // next node after the leaves: same rule as bvh_step
@@ -1085,27 +1056,7 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
         }
         if (model_done) {
             state = 1;
-            if ((F & 32) && any) {
-                // Grid semantics without the walk: the reference's result for this model is
-                // the closest member when no other member lies within `reach` of it and its
-                // hit point is safely inside its own voxel box; else the full
-                // grid_hitset tiers run for this ray in k_trace_deferred.
-                const ModelRec& M = models[im];
-                bool ok = t2 > best + mreach;
-                const f3 ps = o + d * best;
-                const float fx = (ps.x - M.bbox[0] + kEps) / M.vw[0];
-                const float fy = (ps.y - M.bbox[1] + kEps) / M.vw[1];
-                const float fz = (ps.z - M.bbox[2] + kEps) / M.vw[2];
-                constexpr float m = 1e-3f;
-                ok = ok && fx >= (float)(vlo1 & 1023) + m && fx <= (float)((vhi1 & 1023) + 1) - m;
-                ok = ok && fy >= (float)((vlo1 >> 10) & 1023) + m && fy <= (float)(((vhi1 >> 10) & 1023) + 1) - m;
-                ok = ok && fz >= (float)((vlo1 >> 20) & 1023) + m && fz <= (float)(((vhi1 >> 20) & 1023) + 1) - m;
-                if (!ok) {
-                    p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
-                    state = 0;
-                }
-            }
-            if (state == 1 && any) {
+            if (any) {
                 const float dd = model_hit_dist(models[im], o, d, best, ow);
                 if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
             }
@@ -1119,271 +1070,6 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
         atomicAdd(p.segments + 16 + kMaxBounceCounters, it_node);
         atomicAdd(p.segments + 17 + kMaxBounceCounters, it_leaf);
         atomicAdd(p.segments + 19 + kMaxBounceCounters, it_sel);
-    }
-}
-
-// Persistent grid_fast trace for one bounce: computeRayGridIntersection
-// results (Renderer.cpp:238-360, via the BLAS hit set as in grid_hitset) for
-// every live slot, written to the hit buffer.  Per lane: model select ->
-// bounded collection (node visits and leaf triangles as separate steps) ->
-// DDA walk (one voxel per step).  Rays that need more than tier 1 in LDS
-// (hit-set overflow, or a walk that is not provably exact) are deferred to
-// k_trace_deferred, which recomputes them with every tier.
-constexpr int kHitCapT = PT_HITCAP_TRACE;
-
-template <int BS, int F>
-__global__ __launch_bounds__(BS) void k_trace_gf(KParams p, int bounce) {
-    __shared__ int s_stack[kStack * BS];
-    __shared__ int4 s_hs[kHitCapT * BS];
-    int* stack = s_stack + threadIdx.x;
-    int4* hs = s_hs + threadIdx.x;
-    const int n = p.n_live[bounce];
-    const int in_buf = (bounce + 1) & 1;
-    const int lane = threadIdx.x & 63;
-    // lane state: 0 needs a ray, 1 select model, 2 node visit, 4 leaf triangle, 5 walk, 3 no more rays
-    int state = 0;
-    int j = -1;
-    f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
-    float dlen = 0.0f, gdist = kFMax;
-    int gmodel = -1, gtri = -1, im = -1;
-    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), inv = mk3(0, 0, 0), ninv = mk3(0, 0, 0);
-    float t_box = 0.0f, tmin = kFMax, margin = 0.0f;
-    int cur = 0, sp = 0, nh = 0;
-    int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
-    Walk w;
-    w.ix = w.iy = w.iz = w.k = w.ul = w.uh = w.c = w.bk = w.bi = 0;
-    w.tmax = w.delta = mk3(0, 0, 0);
-    w.tested = 0; w.bt = kFMax; w.hit = false;
-    bool exhausted = false;
-    unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
-    unsigned long long it_node = 0, it_leaf = 0, it_walk = 0, it_sel = 0;
-    for (unsigned iters = 0;; iters++) {
-        const unsigned long long idle = __ballot(state == 0);
-        const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (PT_TRACE_STATS && (p.debug & 16)) st_iter++;
-        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
-            const int cnt = __popcll(idle);
-            const int leader = __ffsll((long long)idle) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(p.trace_next, cnt);
-            base = __shfl(base, leader);
-            if (base + cnt >= n) exhausted = true;
-            if (state == 0) {
-                j = base + __popcll(idle & ((1ull << lane) - 1ull));
-                if (j < n) {
-                    const int src = slot_source(p, j);
-                    const float4 a = p.ray[in_buf][0][src];
-                    const float4 b = p.ray[in_buf][1][src];
-                    ow = mk3(a.x, a.y, a.z);
-                    dw = mk3(b.x, b.y, b.z);
-                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
-                    dlen = sqrtf(dot(dw, dw));
-                    gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                    state = 1;
-                } else {
-                    state = 3;
-                }
-            }
-        }
-        if (exhausted && state == 0) state = 3;
-        if (__ballot(state != 3) == 0) break;
-        if (iters > (1u << 26)) {                       // safety net: never spin forever
-            if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
-            break;
-        }
-        int phase = 15;
-        if (F & 8) {
-            const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
-                      c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5));
-            phase = 2; int cm = c2;
-            if (c4 > cm) { phase = 4; cm = c4; }
-            if (c5 > cm) { phase = 8; cm = c5; }
-            if (c1 > cm) { phase = 1; cm = c1; }
-        }
-        if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
-            if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
-            if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
-            if (phase & 8) { st_walk += __popcll(__ballot(state == 5)); it_walk++; }
-            if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
-        }
-        if ((phase & 1) && state == 1) {
-            for (;;) {
-                if (PT_TRACE_STATS && (p.debug & 16)) atomicAdd(p.segments + 13 + kMaxBounceCounters, 1ull);
-                im++;
-                if (im >= p.nmodels) {
-                    const Hit h = make_hit(p, gdist, gmodel, gtri);
-                    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
-                    p.hitm[j] = h.model;
-                    state = 0;
-                    break;
-                }
-                const ModelRec& M = p.models[im];
-                if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
-                o = xform12(M.w2m, ow, 1.0f);
-                d = normalize(xform12(M.w2m, dw, 0.0f));
-                inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
-                if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
-                const f3 pt = o + d * t_box;
-                if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
-                ninv = node_inv(inv);
-                margin = M.wdelta + M.reach;
-                cur = M.bvh_root;
-                sp = 0;
-                nh = 0;
-                tmin = kFMax;
-                state = 2;
-                break;
-            }
-        }
-        bool collected = false;
-        if ((phase & 4) && state == 4) {                // one leaf triangle of the bounded collection
-            const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
-            float t;
-            if (tri_test_rec(A, B, C, o, d, t)) {
-                if (t < tmin) tmin = t;
-                if (!(t > tmin + margin)) {
-                    if (nh == kHitCapT) {                   // drop members now beyond the bound
-                        int wn = 0;
-                        for (int q = 0; q < nh; q++) {
-                            const int4 e = hs[q * BS];
-                            if (!(__int_as_float(e.x) > tmin + margin)) hs[(wn++) * BS] = e;
-                        }
-                        nh = wn;
-                    }
-                    if (nh == kHitCapT) {                   // overflow: defer the whole ray
-                        p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
-                        state = 0;
-                    } else {
-                        hs[nh * BS] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
-                                                __float_as_int(C.w));
-                        nh++;
-                    }
-                }
-            }
-            if (state == 4) {
-                lf_i++;
-                if (lf_i == lf_e) {
-                    if (lf2_i < lf2_e) {
-                        lf_i = lf2_i; lf_e = lf2_e;
-                        lf2_i = lf2_e = 0;
-                    } else if (lf_next >= 0) {
-                        cur = lf_next;
-                        state = 2;
-                    } else if (sp == 0) {
-                        collected = true;
-                    } else {
-                        sp--;
-                        cur = stack[sp * BS];
-                        state = 2;
-                    }
-                }
-            }
-        } else if ((phase & 2) && state == 2) {         // one node of the bounded collection
-            const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-            const float4 q0 = nodes[4 * cur + 0];
-            const float4 q1 = nodes[4 * cur + 1];
-            const float4 q2 = nodes[4 * cur + 2];
-            const float4 q3 = nodes[4 * cur + 3];
-            const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-            const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-            const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-            const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-            float tn0, tf0, tn1, tf1;
-            node_slab(lo0, hi0, o, ninv, tn0, tf0);
-            node_slab(lo1, hi1, o, ninv, tn1, tf1);
-            const float bound = tmin + margin;
-            const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bound;
-            const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bound;
-            const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
-            const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
-            int next = -1;
-            if (i0 && i1) {
-                const bool first0 = tn0 <= tn1;
-                stack[sp * BS] = first0 ? link1 : link0;
-                sp++;
-                next = first0 ? link0 : link1;
-            } else if (i0) {
-                next = link0;
-            } else if (i1) {
-                next = link1;
-            }
-            if (l0 || l1) {
-                lf_i = l0 ? link0 : link1;
-                lf_e = lf_i + (l0 ? cnt0 : cnt1);
-                lf2_i = (l0 && l1) ? link1 : 0;
-                lf2_e = (l0 && l1) ? link1 + cnt1 : 0;
-                lf_next = next;
-                state = 4;
-            } else if (next >= 0) {
-                cur = next;
-            } else if (sp == 0) {
-                collected = true;
-            } else {
-                sp--;
-                cur = stack[sp * BS];
-            }
-        }
-        if (collected) {
-            if (nh == 0) {
-                state = 1;                              // no accepted triangle on the ray: no hit voxel
-            } else {
-                walk_init(p, p.models[im], d, inv, o + d * t_box, w);
-                walk_union<BS>(hs, nh, w);
-                state = 5;
-            }
-        } else if ((phase & 8) && state == 5) {
-            // several voxels per iteration: a walk step is cheap next to the loop's own overhead
-            bool ended = false;
-            for (int q = 0; q < PT_WALK_BURST && !ended; q++) ended = walk_step<BS>(p, d, hs, nh, tmin, w);
-            if (ended) {
-                const ModelRec& M = p.models[im];
-                const bool final_min = w.bk >= 0 && w.bt == tmin && t_box + w.tbe < tmin + M.wdelta;
-                const float tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
-                if (final_min || tw < tmin + M.wdelta) {
-                    if (w.hit) {
-                        const float best = w.bk >= 0 ? w.bt : kFMax;
-                        const float dd = model_hit_dist(M, o, d, best, ow);
-                        if (gdist > dd) { gdist = dd; gmodel = im; gtri = w.bk >= 0 ? w.bi : -1; }
-                    }
-                    state = 1;
-                } else {                                // tier 1 not provably exact: defer the ray
-                    p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
-                    state = 0;
-                }
-            }
-        }
-    }
-    if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
-        atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
-        atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
-        atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
-        atomicAdd(p.segments + 11 + kMaxBounceCounters, st_walk);
-        atomicAdd(p.segments + 12 + kMaxBounceCounters, st_sel);
-        atomicAdd(p.segments + 16 + kMaxBounceCounters, it_node);
-        atomicAdd(p.segments + 17 + kMaxBounceCounters, it_leaf);
-        atomicAdd(p.segments + 18 + kMaxBounceCounters, it_walk);
-        atomicAdd(p.segments + 19 + kMaxBounceCounters, it_sel);
-    }
-}
-
-// Rays k_trace_gf deferred: the full grid_hitset tiers (LDS, global pool,
-// list-walking DDA), one lane per ray.
-template <int BS>
-__global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
-    __shared__ int s_stack[kStack * BS];
-    __shared__ int4 s_hs[kHitCap * BS];
-    const int in_buf = (bounce + 1) & 1;
-    const int cnt = *p.defer_count;
-    if ((PT_TRACE_STATS && (p.debug & 16)) && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
-    for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
-        const int j = p.defer_slots[q];
-        const int src = slot_source(p, j);
-        const float4 a = p.ray[in_buf][0][src];
-        const float4 b = p.ray[in_buf][1][src];
-        const Hit h = intersect_scene<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
-                                                           s_stack + threadIdx.x, s_hs + threadIdx.x);
-        p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
-        p.hitm[j] = h.model;
     }
 }
 
@@ -1543,7 +1229,6 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
-        *p.defer_count = 0;
     }
 }
 
@@ -1676,10 +1361,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     {
         // Persistent trace (ACCEL_BVH): hit buffer + work counter; PT_TRACE_SPLIT=0 keeps the fused kernel.
         const char* e = std::getenv("PT_TRACE_SPLIT");
-        // default: on for ACCEL_BVH; opt-in (PT_TRACE_SPLIT=1) for ACCEL_GRID_FAST, where the
-        // persistent kernel is still slower than the fused one
-        const int want = e ? std::atoi(e) : (cfg.accel == ACCEL_BVH ? 1 : 0);
-        split_trace = (cfg.accel == ACCEL_BVH || cfg.accel == ACCEL_GRID_FAST) && want != 0;
+        // ACCEL_BVH only: for ACCEL_GRID_FAST the fused kernel measured faster than every
+        // split variant tried
+        split_trace = cfg.accel == ACCEL_BVH && !(e && std::atoi(e) == 0);
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
@@ -1687,7 +1371,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
-        const int w = wpc ? std::max(1, std::atoi(wpc)) : (cfg.accel == ACCEL_GRID_FAST ? 16 : 20);   // resident waves per CU
+        const int w = wpc ? std::max(1, std::atoi(wpc)) : 20;   // resident waves per CU
         trace_blocks = std::max(1, cus) * w;
         const size_t hcap = split_trace ? cap : 1;
         // 4-wide traversal pushes up to 3 entries per level: LDS holds kStack, the rest spills
@@ -1701,9 +1385,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
         PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.trace_next, nullptr, sizeof(int), stream));
-        PT_HIP(upload(allocs, &kp.defer_slots, nullptr, hcap * sizeof(int), stream));
-        PT_HIP(upload(allocs, &kp.defer_count, nullptr, sizeof(int), stream));
-        PT_HIP(hipMemsetAsync(kp.defer_count, 0, sizeof(int), stream));
+
         PT_HIP(hipMemsetAsync(kp.trace_next, 0, sizeof(int), stream));
     }
     PT_HIP(upload(allocs, &kp.segments, nullptr, (32 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
@@ -1736,12 +1418,6 @@ int Renderer::launchPrimary() {
 
 void Renderer::launchTrace(int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
-    if (cfg.accel == ACCEL_GRID_FAST) {
-        if (kp.trace_flags & 32) hipLaunchKernelGGL((k_trace_bvh<64, 43>), g, t, 0, stream, kp, b);
-        else if (kp.trace_flags & 8) hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b);
-        else hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, stream, kp, b);
-        return;
-    }
     switch (kp.trace_flags & 31) {
         case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, stream, kp, b); break;
         case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, stream, kp, b); break;
@@ -1812,10 +1488,6 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
             if (b > 0 && split_trace) {
                 launchTrace(b);
-                if (cfg.accel == ACCEL_GRID_FAST) {
-                    PT_HIP(hipGetLastError());
-                    hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)trace_blocks), dim3(64), 0, stream, kp, b);
-                }
                 PT_HIP(hipGetLastError());
                 if (profiling) {
                     hipEventRecord(e1, stream);
