@@ -31,6 +31,9 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP
 #define PT_HITCAP 6
 #endif
+#ifndef PT_WALK_SKIP
+#define PT_WALK_SKIP 1        // fast-forward the grid_fast walk to the members' union box (walk_skip)
+#endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
 #endif
@@ -282,7 +285,9 @@ __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 i
     int sp = 0;
     int cur = M.bvh_root;
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+    unsigned nvis = 0;
     for (;;) {
+        nvis++;
         const float4 q0 = nodes[4 * cur + 0];
         const float4 q1 = nodes[4 * cur + 1];
         const float4 q2 = nodes[4 * cur + 2];
@@ -345,6 +350,10 @@ __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 i
             cur = stack[sp * STRIDE];
         }
     }
+    if (PT_TRACE_STATS && (p.debug & 4)) {          // collection statistics: node visits, collections
+        atomicAdd(p.segments + 22 + kMaxBounceCounters, (unsigned long long)nvis);
+        atomicAdd(p.segments + 23 + kMaxBounceCounters, 1ull);
+    }
     *tmin_out = tmin;
     return nh;
 }
@@ -382,6 +391,7 @@ struct Walk {
     bool hit;
     float te;                      // entry parameter (from pt) of the current voxel
     float tbe;                     // entry parameter of the voxel where the current best was tested
+    bool passed;                   // stopped because the walk left the union box (not a reference stop)
 };
 
 __device__ __forceinline__ void walk_init(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, Walk& w) {
@@ -410,6 +420,7 @@ __device__ __forceinline__ void walk_init(const KParams& p, const ModelRec& M, f
     w.hit = false;
     w.te = 0.0f;
     w.tbe = 0.0f;
+    w.passed = false;
 }
 
 template <int HSTRIDE>
@@ -422,6 +433,75 @@ __device__ __forceinline__ void walk_union(const int4* __restrict__ hs, int nh, 
     }
     w.ul = ulx | (uly << 10) | (ulz << 20);
     w.uh = uhx | (uhy << 10) | (uhz << 20);
+}
+
+// Fast-forward of the walk to its first voxel inside the members' union box.
+// Before that voxel nothing can happen: no voxel outside the union box is a hit
+// voxel, and the reference walk cannot stop before its first hit voxel.  The
+// DDA's voxel order is the merge of the three per-axis crossing sequences
+// tmax_a, tmax_a + delta_a, ... (each sum rounded as the walk rounds it) by
+// (value, axis priority z < y < x) -- exactly the walk's
+// "x if tmax.x < tmax.y && tmax.x < tmax.z, else y if tmax.y < tmax.z, else z"
+// choice -- so the state at entry (indices, tmax, step count k, entry
+// parameter te) follows from per-axis running sums, one add per skipped step
+// instead of one full walk_step.  Leaves the walk untouched when it is already
+// in range on every axis, when an axis leaves its range before the entry
+// (the plain walk then stops there), or for zero / huge direction slopes.
+__device__ __forceinline__ void walk_skip(f3 d, Walk& w) {
+    const float dd[3] = {d.x, d.y, d.z};
+    const float t0[3] = {w.tmax.x, w.tmax.y, w.tmax.z};
+    const float dl[3] = {w.delta.x, w.delta.y, w.delta.z};
+    const int ii[3] = {w.ix, w.iy, w.iz};
+    int need[3], over[3];
+    bool go = false;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const int lo = (w.ul >> (10 * a)) & 1023, hi = (w.uh >> (10 * a)) & 1023;
+        if (dd[a] == 0.0f || !(absr(t0[a]) < 1e30f) || !(dl[a] < 1e30f)) return;
+        need[a] = dd[a] > 0.0f ? max(0, lo - ii[a]) : max(0, ii[a] - hi);
+        over[a] = dd[a] > 0.0f ? hi - ii[a] + 1 : ii[a] - lo + 1;
+        if (over[a] <= 0) return;                       // already past the range: the walk stops at once
+        go = go || need[a] > 0;
+    }
+    if (!go) return;
+    // crossing value of the last step each axis needs; the entry step is their
+    // maximum by (value, priority), priority z = 0 < y = 1 < x = 2
+    float kn[3];
+    int A = -1;
+    float T = 0.0f;
+#pragma unroll
+    for (int a = 2; a >= 0; a--) {                      // z first, so a later axis wins only when strictly greater
+        float K = t0[a];
+        for (int c = 1; c < need[a]; c++) K += dl[a];
+        kn[a] = K;
+        const int pa = 2 - a;
+        if (need[a] > 0 && (A < 0 || K > T || (K == T && pa > 2 - A))) { A = a; T = K; }
+    }
+    const int pA = 2 - A;
+    int cnt[3];
+    float nxt[3];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        if (b == A) { cnt[b] = need[b]; nxt[b] = kn[b] + dl[b]; continue; }
+        int c = 0;
+        float K = t0[b];
+        if (need[b] > 0) { c = need[b] - 1; K = kn[b]; }
+        const int pb = 2 - b;
+        // count b's steps before the entry step
+        while (K < T || (K == T && pb < pA)) {
+            c++;
+            if (c >= over[b]) return;                   // b leaves its range first: plain walk
+            K += dl[b];
+        }
+        cnt[b] = c;
+        nxt[b] = K;
+    }
+    w.ix = ii[0] + (dd[0] > 0.0f ? cnt[0] : -cnt[0]);
+    w.iy = ii[1] + (dd[1] > 0.0f ? cnt[1] : -cnt[1]);
+    w.iz = ii[2] + (dd[2] > 0.0f ? cnt[2] : -cnt[2]);
+    w.tmax = mk3(nxt[0], nxt[1], nxt[2]);
+    w.k = cnt[0] + cnt[1] + cnt[2];
+    w.te = T;
 }
 
 // One voxel of the walk; returns true when the walk has stopped.
@@ -454,7 +534,10 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
     const unsigned long long all = nh >= 64 ? ~0ull : ((1ull << nh) - 1ull);
     if (w.tested == all || (w.bk >= 0 && w.bt == tmin)) return true;
     const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
-    if ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz)) return true;
+    if ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz)) {
+        w.passed = true;
+        return true;
+    }
     if (w.hit) {
         const int cx = w.c & 1023, cy = (w.c >> 10) & 1023, cz = (w.c >> 20) & 1023;
         if (iabs(cx - ix) > 2 || iabs(cy - iy) > 2 || iabs(cz - iz) > 2) return true;
@@ -485,14 +568,29 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
     Walk w;
     walk_init(p, M, d, inv, pt, w);
     walk_union<HSTRIDE>(hs, nh, w);
-    while (!walk_step<HSTRIDE>(p, d, hs, nh, tmin, w)) {}
+#if PT_WALK_SKIP
+    walk_skip(d, w);
+#endif
+    unsigned steps = 1;
+    while (!walk_step<HSTRIDE>(p, d, hs, nh, tmin, w)) steps++;
+    if (PT_TRACE_STATS && (p.debug & 4)) {          // walk statistics: steps, walks, members; steps per model
+        atomicAdd(p.segments + 20 + kMaxBounceCounters, (unsigned long long)steps);
+        atomicAdd(p.segments + 21 + kMaxBounceCounters, 1ull);
+        atomicAdd(p.segments + 24 + kMaxBounceCounters, (unsigned long long)nh);
+        const int mi = (int)(&M - p.models);
+        if (mi >= 0 && mi < 4) atomicAdd(p.segments + 25 + mi + kMaxBounceCounters, (unsigned long long)steps);
+    }
     WalkResult r;
     r.hit = w.hit;
     r.t = w.bt;
     r.tri = w.bi;
     r.has_best = w.bk >= 0;
     r.final_min = w.bk >= 0 && w.bt == tmin && t_box + w.tbe < tmin + win;
-    r.tw = t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
+    // A walk that left the union box before any hit voxel has not stopped in the
+    // reference sense: the reference walk goes on (it cannot stop before a hit
+    // voxel) and may still enter the box of a member beyond the collection
+    // window, so that outcome is final only for an unbounded collection.
+    r.tw = (w.passed && !w.hit) ? 3.0e38f : t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
     return r;
 }
 

@@ -80,6 +80,15 @@ def main():
             out[v]["lanes_per_phase_iter"] = {k: round(b / max(a, 1), 2) for k, (a, b) in ph.items()}
             out[v]["select_loop_trips"] = allc[76]
             out[v]["deferred"] = allc[77]
+        if allc[84]:                                   # PT_TRACE_STATS build, PT_DEBUG_ABLATE & 4
+            segs_all = rs[v].segments()
+            out[v]["walk_steps_per_walk"] = round(allc[83] / allc[84], 2)
+            out[v]["walks_per_segment"] = round(allc[84] / segs_all, 3)
+            out[v]["members_per_walk"] = round(allc[87] / allc[84], 2)
+            out[v]["walk_steps_per_segment_by_model"] = [round(x / segs_all, 2) for x in allc[88:92]]
+        if allc[86]:
+            out[v]["collect_nodes_per_collection"] = round(allc[85] / allc[86], 2)
+            out[v]["collections_per_segment"] = round(allc[86] / rs[v].segments(), 3)
         diag = allc[64:67]
         if any(diag):
             out[v]["diag_tier2_t1overflow_fallback"] = diag

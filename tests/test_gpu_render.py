@@ -263,3 +263,38 @@ def test_trace_kernel_variants_bitexact(gpu, pt_mod, oracle_mod, synth_dir, monk
         img, seg, oimg, oseg = _render_both(P, O, s, cfg)
         assert seg == oseg
         assert_bitexact(img, oimg, "image")
+
+
+def _edge_miss_scene(P):
+    """Triangle A (y = 0) whose left edge lies on a voxel boundary, and a far
+    triangle B (y = 100).  Rays travelling up just left of A's edge pass A's
+    barycentric tolerance test (closest hit) but never enter A's voxel box, so
+    the reference grid walk continues and returns B (OBJ units, x1000 on load)."""
+    pos = np.float32([(0, 0, 0), (10, 0, 0), (0, 0, 10), (-2.5, 100, 3), (2, 100, 3), (-2.5, 100, 8)])
+    nrm = np.float32([(0, 1, 0)] * 3 + [(0, -1, 0)] * 3)
+    s = P.Scene()
+    m = s.addMesh(pos, nrm, np.int32([(0, 1, 2), (3, 4, 5)]))
+    s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.addModel(m, (0.5, 0.5, 0.5), (0, 0, 0), (40000, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.build(bvh=True)
+    return s
+
+
+@pytest.mark.parametrize("accel", [0, 2])
+def test_grid_fast_member_box_missed_far_hit(gpu, pt_mod, oracle_mod, accel):
+    """The walk passes every collected member's voxel box without a hit voxel:
+    the result is final only once no farther (uncollected) member can follow."""
+    P, O = pt_mod, oracle_mod
+    s = _edge_miss_scene(P)
+    xs = np.linspace(-6, -49, 24)
+    o = np.float32([(x, -10000, 5000 + 37 * i) for i, x in enumerate(xs)]
+                   + [(40000 + 0.5 * x, -10000, 2500) for x in xs])
+    d = np.tile(np.float32([-1e-5, 1, 1e-5]), (len(o), 1))
+    r = P.Renderer(P.RenderConfig(width=8, height=8, accel=accel))
+    r.allocateOnGPU(s)
+    t, n, m = r.intersect_rays(o, d)
+    r.free()
+    ot, on, om = O.intersect_rays(flat_from_export(s.export()), o, d, accel=0)
+    assert (ot > 50000).sum() >= 24                  # the reference returns the far triangle
+    assert_bitexact(m, om, "model")
+    assert_bitexact(t, ot, "dist")
