@@ -67,6 +67,8 @@ struct KParams {
     int* trace_next;                    // persistent trace: next unclaimed source block, reset by k_scan
     int trace_refill;                   // refill a wave's idle lanes once this many are idle
     int trace_flags;                    // k_trace_bvh variant: 1 LDS model records, 2 leaf steps, 4 block claims
+    int* defer_slots;                   // k_trace_gf: slots whose hit set overflowed LDS (k_trace_deferred)
+    int* defer_count;                   // reset by k_scan
 };
 
 constexpr int kMaxBounceCounters = 64;
@@ -119,8 +121,9 @@ private:
     bool profiling = false;
     std::vector<void*> allocs;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events, trace_events;
-    bool split_trace = false;        // ACCEL_BVH: persistent k_trace_bvh + shading pass
+    bool split_trace = false;        // persistent k_trace_bvh / k_trace_gf + shading pass
     int trace_blocks = 0;
+    int gf_flags = 9;                // k_trace_gf variant: 1 LDS model records, 8 phase scheduling
     KernelStats stats;
 };
 

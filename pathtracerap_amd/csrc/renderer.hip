@@ -423,16 +423,25 @@ __device__ __forceinline__ void walk_init(const KParams& p, const ModelRec& M, f
     w.passed = false;
 }
 
-template <int HSTRIDE>
-__device__ __forceinline__ void walk_union(const int4* __restrict__ hs, int nh, Walk& w) {
+// Union of the members' voxel boxes.  CAP > 0: members come from a
+// register array through `get` (fully unrolled, constant indices).
+template <int CAP, class GetM>
+__device__ __forceinline__ void walk_union_g(GetM get, int nh, Walk& w) {
     int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
-    for (int h = 0; h < nh; h++) {
-        const int4 e = hs[h * HSTRIDE];
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 e = get(h);
         ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
         uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
     }
     w.ul = ulx | (uly << 10) | (ulz << 20);
     w.uh = uhx | (uhy << 10) | (uhz << 20);
+}
+
+template <int HSTRIDE>
+__device__ __forceinline__ void walk_union(const int4* __restrict__ hs, int nh, Walk& w) {
+    walk_union_g<0>([&](int h) { return hs[h * HSTRIDE]; }, nh, w);
 }
 
 // Fast-forward of the walk to its first voxel inside the members' union box.
@@ -504,17 +513,19 @@ __device__ __forceinline__ void walk_skip(f3 d, Walk& w) {
     w.te = T;
 }
 
-// One voxel of the walk; returns true when the walk has stopped.
-template <int HSTRIDE>
-__device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __restrict__ hs, int nh, float tmin,
-                                          Walk& w) {
+// One voxel of the walk; returns true when the walk has stopped.  Members
+// through `get`; CAP > 0: a register array of CAP entries (unrolled).
+template <int CAP, class GetM>
+__device__ __forceinline__ bool walk_step_g(const KParams& p, f3 d, GetM get, int nh, float tmin, Walk& w) {
     const int ulx = w.ul & 1023, uly = (w.ul >> 10) & 1023, ulz = (w.ul >> 20) & 1023;
     const int uhx = w.uh & 1023, uhy = (w.uh >> 10) & 1023, uhz = (w.uh >> 20) & 1023;
     const int ix = w.ix, iy = w.iy, iz = w.iz, k = w.k;
     bool vhit = false;
     if (ix >= ulx && ix <= uhx && iy >= uly && iy <= uhy && iz >= ulz && iz <= uhz) {
-        for (int h = 0; h < nh; h++) {
-            const int4 e = hs[h * HSTRIDE];
+#pragma unroll
+        for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+            if (CAP > 0 && h >= nh) break;
+            const int4 e = get(h);
             if (vbox_has(e.z, e.w, ix, iy, iz)) {
                 vhit = true;
                 if (!((w.tested >> h) & 1ull)) {
@@ -563,16 +574,34 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
 }
 
 template <int HSTRIDE>
-__device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
-                                  const int4* __restrict__ hs, int nh, float tmin, float win) {
+__device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __restrict__ hs, int nh, float tmin,
+                                          Walk& w) {
+    return walk_step_g<0>(p, d, [&](int h) { return hs[h * HSTRIDE]; }, nh, tmin, w);
+}
+
+template <int CAP, class GetM>
+__device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
+                                                    GetM get, int nh, float tmin, float win) {
+    const bool stamps = PT_TRACE_STATS && (p.debug & 64);     // wave cycles: init+union, skip, steps
+    unsigned long long c0 = stamps ? clock64() : 0;
     Walk w;
     walk_init(p, M, d, inv, pt, w);
-    walk_union<HSTRIDE>(hs, nh, w);
+    walk_union_g<CAP>(get, nh, w);
+    unsigned long long c1 = stamps ? clock64() : 0;
 #if PT_WALK_SKIP
     walk_skip(d, w);
 #endif
+    unsigned long long c2 = stamps ? clock64() : 0;
     unsigned steps = 1;
-    while (!walk_step<HSTRIDE>(p, d, hs, nh, tmin, w)) steps++;
+    while (!walk_step_g<CAP>(p, d, get, nh, tmin, w)) steps++;
+    if (stamps) {
+        const unsigned long long c3 = clock64();
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+            atomicAdd(p.segments + 29 + kMaxBounceCounters, c1 - c0);
+            atomicAdd(p.segments + 30 + kMaxBounceCounters, c2 - c1);
+            atomicAdd(p.segments + 31 + kMaxBounceCounters, c3 - c2);
+        }
+    }
     if (PT_TRACE_STATS && (p.debug & 4)) {          // walk statistics: steps, walks, members; steps per model
         atomicAdd(p.segments + 20 + kMaxBounceCounters, (unsigned long long)steps);
         atomicAdd(p.segments + 21 + kMaxBounceCounters, 1ull);
@@ -592,6 +621,24 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
     // window, so that outcome is final only for an unbounded collection.
     r.tw = (w.passed && !w.hit) ? 3.0e38f : t_box + fminf(fminf(w.tmax.x, w.tmax.y), w.tmax.z);
     return r;
+}
+
+template <int HSTRIDE>
+__device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
+                                  const int4* __restrict__ hs, int nh, float tmin, float win) {
+    return hitset_walk_g<0>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * HSTRIDE]; }, nh, tmin, win);
+}
+
+// The same walk over at most CAP members copied to registers first: the walk's
+// per-voxel membership tests then wait on no LDS reads.
+template <int CAP, int HSTRIDE>
+__device__ __forceinline__ WalkResult hitset_walk_regs(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt,
+                                                       float t_box, const int4* __restrict__ hs, int nh, float tmin,
+                                                       float win) {
+    int4 mem[CAP];
+#pragma unroll
+    for (int h = 0; h < CAP; h++) mem[h] = h < nh ? hs[h * HSTRIDE] : make_int4(0, 0, 0, 0);
+    return hitset_walk_g<CAP>(p, M, d, inv, pt, t_box, [&](int h) { return mem[h]; }, nh, tmin, win);
 }
 
 // Overflow tiers of grid_hitset: bounded, then unbounded collection into a
@@ -842,14 +889,14 @@ __device__ __forceinline__ int slot_source(const KParams& p, int j) {
 // Every wave exits once all blocks are claimed and its lanes are idle.
 // Per-lane traversal stack: kStack entries in LDS (lane-contiguous), deeper
 // entries in a global spill area laid out lane-minor (p.spill_stride lanes).
-template <int BS>
+template <int BS, int SCAP = kStack>
 __device__ __forceinline__ void spush_t(int* stack, int* spill, int stride, int sp, int e) {
-    if (sp < kStack) stack[sp * BS] = e;
-    else spill[(size_t)(sp - kStack) * stride] = e;
+    if (sp < SCAP) stack[sp * BS] = e;
+    else spill[(size_t)(sp - SCAP) * stride] = e;
 }
-template <int BS>
+template <int BS, int SCAP = kStack>
 __device__ __forceinline__ int spop_t(const int* stack, const int* spill, int stride, int sp) {
-    return sp < kStack ? stack[sp * BS] : spill[(size_t)(sp - kStack) * stride];
+    return sp < SCAP ? stack[sp * BS] : spill[(size_t)(sp - SCAP) * stride];
 }
 #define spush(stack, spill, sp, e) spush_t<BS>(stack, spill, p.spill_stride, sp, e)
 #define spop(stack, spill, sp) spop_t<BS>(stack, spill, p.spill_stride, sp)
@@ -1171,6 +1218,330 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
     }
 }
 
+// Persistent grid_fast trace for one bounce: the results of
+// computeRayGridIntersection (Renderer.cpp:238-360) computed as grid_hitset
+// does, for every live slot, written to the hit buffer the shading pass reads.
+// Same skeleton as k_trace_bvh: each lane advances its own ray one step per
+// loop iteration -- select the next model (instance culling, model-space
+// transform, the grid's bounding-box entry test), visit one BLAS node of the
+// bounded hit-set collection, test one leaf triangle, or run the whole DDA walk
+// of a collected hit set (fast-forwarded to the members' union box, so a walk
+// is a few voxels) -- and the wave runs only the step kind most lanes wait in.
+// A walk that is not provably exact restarts the collection with the next
+// tier's window (W, 2R, unbounded), in place.  A hit set that overflows the
+// kGfHitCap LDS entries defers the whole ray to k_trace_deferred (the fused
+// path's tiers with the global pool).  LDS per lane: kGfStack stack entries
+// (deeper entries spill to global memory) + kGfHitCap hit-set members.
+#ifndef PT_GF_STACK
+#define PT_GF_STACK 12
+#endif
+#ifndef PT_GF_HITCAP
+#define PT_GF_HITCAP 4
+#endif
+#ifndef PT_GF_MINWAVES
+#define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
+#endif
+constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
+
+template <int BS, int F>
+__global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce) {
+    __shared__ int s_stack[kGfStack * BS];
+    __shared__ int4 s_hs[kGfHitCap * BS];
+    __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
+    int* stack = s_stack + threadIdx.x;
+    int4* hs = s_hs + threadIdx.x;
+    int* spill = p.spill + (size_t)blockIdx.x * BS + threadIdx.x;
+    const bool lds_models = (F & 1) && p.nmodels <= kLdsModels;
+    if (lds_models) {
+        const int* src = reinterpret_cast<const int*>(p.models);
+        int* dst = reinterpret_cast<int*>(s_models);
+        const int nw = p.nmodels * (int)(sizeof(ModelRec) / 4);
+        for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
+        __syncthreads();
+    }
+    const ModelRec* models = lds_models ? s_models : p.models;
+    const int n = p.n_live[bounce];
+    const int in_buf = (bounce + 1) & 1;
+    const int lane = threadIdx.x & 63;
+    // lane state: 0 needs a ray, 1 select model, 2 node visit, 4 leaf triangle, 5 walk, 3 no more rays
+    int state = 0;
+    int j = -1;
+    f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
+    float dlen = 0.0f, gdist = kFMax;
+    int gmodel = -1, gtri = -1, im = -1;
+    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), inv = mk3(0, 0, 0);
+    float t_box = 0.0f, tmin = kFMax, margin = 0.0f;
+    int cur = 0, sp = 0, nh = 0, tier = 0;
+    int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
+    int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
+    bool exhausted = false;
+    unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
+    unsigned long long it_node = 0, it_leaf = 0, it_walk = 0, it_sel = 0;
+    unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
+    const bool stamps = PT_TRACE_STATS && (p.debug & 32);
+    unsigned long long ts = stamps ? clock64() : 0;
+    for (unsigned iters = 0;; iters++) {
+        const unsigned long long idle = __ballot(state == 0);
+        const unsigned long long busy = __ballot(state != 0 && state != 3);
+        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+            const int cnt = __popcll(idle);
+            const int leader = __ffsll((long long)idle) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.trace_next, cnt);
+            base = __shfl(base, leader);
+            if (base + cnt >= n) exhausted = true;
+            if (state == 0) {
+                j = base + __popcll(idle & ((1ull << lane) - 1ull));
+                if (j < n) {
+                    const int src = slot_source(p, j);
+                    const float4 a = p.ray[in_buf][0][src];
+                    const float4 b = p.ray[in_buf][1][src];
+                    ow = mk3(a.x, a.y, a.z);
+                    dw = mk3(b.x, b.y, b.z);
+                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                    dlen = sqrtf(dot(dw, dw));
+                    gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
+                    state = 1;
+                } else {
+                    state = 3;
+                }
+            }
+        }
+        if (exhausted && state == 0) state = 3;
+        if (__ballot(state != 3) == 0) break;
+        if (iters > (1u << 26)) {                       // safety net: never spin forever
+            if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
+            break;
+        }
+        int phase = 15;
+        if (F & 8) {
+            const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
+                      c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5));
+            phase = 2; int cm = c2;
+            if (c4 > cm) { phase = 4; cm = c4; }
+            if (c5 > cm) { phase = 8; cm = c5; }
+            if (c1 > cm) { phase = 1; cm = c1; }
+        }
+        if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
+            st_iter++;
+            if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
+            if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
+            if (phase & 8) { st_walk += __popcll(__ballot(state == 5)); it_walk++; }
+            if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
+        }
+        if (stamps) { const unsigned long long t = clock64(); cy[0] += t - ts; ts = t; }
+        if ((phase & 1) && state == 1) {                // next model that survives culling and the grid entry test
+            for (;;) {
+                im++;
+                if (im >= p.nmodels) {
+                    Hit h;
+                    h.dist = kFMax; h.n = mk3(0, 0, 0); h.model = -1;
+                    if (gdist < kFMax) {
+                        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
+                        h.dist = gdist;
+                        h.model = gmodel;
+                        h.n = normalize(xform_normal9(models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
+                    }
+                    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+                    p.hitm[j] = h.model;
+                    state = 0;
+                    break;
+                }
+                const ModelRec& M = models[im];
+                if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
+                o = xform12(M.w2m, ow, 1.0f);
+                d = normalize(xform12(M.w2m, dw, 0.0f));
+                inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+                if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
+                const f3 pt = o + d * t_box;
+                if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
+                tier = 0;
+                margin = M.wdelta + M.reach;
+                cur = M.bvh_root;
+                sp = 0; nh = 0; tmin = kFMax; pblk = -1;
+                state = 2;
+                break;
+            }
+        }
+        if (stamps) { const unsigned long long t = clock64(); cy[1] += t - ts; ts = t; }
+        bool collected = false;
+        if ((phase & 4) && state == 4) {                // one leaf triangle of the collection
+            const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
+            float t;
+            if (tri_test_rec(A, B, C, o, d, t)) {
+                if (t < tmin) tmin = t;
+                if (!(t > tmin + margin)) {             // required member (NaN is kept)
+                    const int4 e = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
+                                             __float_as_int(C.w));
+                    if (pblk < 0) {
+                        if (nh == kGfHitCap) {          // drop members now beyond the bound
+                            int wn = 0;
+                            for (int q = 0; q < nh; q++) {
+                                const int4 x = hs[q * BS];
+                                if (!(__int_as_float(x.x) > tmin + margin)) hs[(wn++) * BS] = x;
+                            }
+                            nh = wn;
+                        }
+                        if (nh == kGfHitCap) {          // LDS full: continue in a 64-member global pool block
+                            const int blk = atomicAdd(p.hs_pool_next, 1);
+                            if (blk < p.hs_pool_blocks) {
+                                pblk = blk;
+                                int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
+                                for (int q = 0; q < nh; q++) g[q] = hs[q * BS];
+                            }
+                        }
+                    }
+                    if (pblk >= 0) {
+                        int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
+                        if (nh == kHitCapPool) {
+                            int wn = 0;
+                            for (int q = 0; q < nh; q++) {
+                                const int4 x = g[q];
+                                if (!(__int_as_float(x.x) > tmin + margin)) g[wn++] = x;
+                            }
+                            nh = wn;
+                        }
+                        if (nh < kHitCapPool) g[nh++] = e;
+                        else { p.defer_slots[atomicAdd(p.defer_count, 1)] = j; state = 0; }   // pool block full too
+                    } else if (nh < kGfHitCap) {
+                        hs[nh * BS] = e;
+                        nh++;
+                    } else {                            // pool exhausted: the whole ray goes to k_trace_deferred
+                        p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                        state = 0;
+                    }
+                }
+            }
+            if (state == 4) {
+                lf_i++;
+                if (lf_i == lf_e) {
+                    if (lf2_i < lf2_e) {
+                        lf_i = lf2_i; lf_e = lf2_e;
+                        lf2_i = lf2_e = 0;
+                    } else if (lf_next >= 0) {
+                        cur = lf_next;
+                        state = 2;
+                    } else if (sp == 0) {
+                        collected = true;
+                    } else {
+                        sp--;
+                        cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
+                        state = 2;
+                    }
+                }
+            }
+        } else if ((phase & 2) && state == 2) {         // one node of the collection (bound t_min + margin)
+            const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+            const float4 q0 = nodes[4 * cur + 0];
+            const float4 q1 = nodes[4 * cur + 1];
+            const float4 q2 = nodes[4 * cur + 2];
+            const float4 q3 = nodes[4 * cur + 3];
+            const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+            const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+            const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+            const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+            const f3 ninv = node_inv(inv);
+            float tn0, tf0, tn1, tf1;
+            node_slab(lo0, hi0, o, ninv, tn0, tf0);
+            node_slab(lo1, hi1, o, ninv, tn1, tf1);
+            const float bound = tmin + margin;
+            const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bound;
+            const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bound;
+            const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
+            const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
+            int next = -1;
+            if (i0 && i1) {
+                const bool first0 = tn0 <= tn1;         // near child first tightens the bound
+                spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, first0 ? link1 : link0);
+                sp++;
+                next = first0 ? link0 : link1;
+            } else if (i0) {
+                next = link0;
+            } else if (i1) {
+                next = link1;
+            }
+            if (l0 || l1) {                             // leaf 0, then leaf 1, then `next`
+                lf_i = l0 ? link0 : link1;
+                lf_e = lf_i + (l0 ? cnt0 : cnt1);
+                lf2_i = (l0 && l1) ? link1 : 0;
+                lf2_e = (l0 && l1) ? link1 + cnt1 : 0;
+                lf_next = next;
+                state = 4;
+            } else if (next >= 0) {
+                cur = next;
+            } else if (sp == 0) {
+                collected = true;
+            } else {
+                sp--;
+                cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
+            }
+        }
+        if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
+        if (collected) {
+            // no accepted triangle anywhere on the ray (the first tier's bound is open
+            // until the first member): no hit voxel, the model is missed
+            state = nh == 0 ? 1 : 5;
+        } else if ((phase & 8) && state == 5) {          // the whole walk of the collected hit set
+            const ModelRec& M = models[im];
+            const float win = tier == 0 ? M.wdelta : (tier == 1 ? 2.0f * M.reach : 3.0e38f);
+            const f3 pt = o + d * t_box;
+            const WalkResult w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
+                                          : hitset_walk<1>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool,
+                                                           nh, tmin, win);
+            if (tier == 2 || w.final_min || w.tw < tmin + win) {
+                if (w.hit && w.has_best) {
+                    const float dd = model_hit_dist(M, o, d, w.t, ow);
+                    if (gdist > dd) { gdist = dd; gmodel = im; gtri = w.tri; }
+                }
+                state = 1;
+            } else {                                    // not provably exact: next tier's collection
+                tier++;
+                margin = tier == 1 ? 3.0f * M.reach : 3.0e38f;
+                cur = M.bvh_root;
+                sp = 0; nh = 0; tmin = kFMax;
+                state = 2;
+            }
+        }
+        if (stamps) { const unsigned long long t = clock64(); cy[4] += t - ts; ts = t; }
+    }
+    if (stamps && lane == 0)
+        for (int q = 0; q < 5; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
+    if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
+        atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
+        atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
+        atomicAdd(p.segments + 11 + kMaxBounceCounters, st_walk);
+        atomicAdd(p.segments + 12 + kMaxBounceCounters, st_sel);
+        atomicAdd(p.segments + 16 + kMaxBounceCounters, it_node);
+        atomicAdd(p.segments + 17 + kMaxBounceCounters, it_leaf);
+        atomicAdd(p.segments + 18 + kMaxBounceCounters, it_walk);
+        atomicAdd(p.segments + 19 + kMaxBounceCounters, it_sel);
+    }
+}
+
+// Rays k_trace_gf deferred (LDS hit-set overflow): the fused path's
+// intersect_scene<ACCEL_GRID_FAST> (LDS tiers, global pool, list-walking DDA),
+// one lane per ray.
+template <int BS>
+__global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
+    __shared__ int s_stack[kStack * BS];
+    __shared__ int4 s_hs[kHitCap * BS];
+    const int in_buf = (bounce + 1) & 1;
+    const int cnt = *p.defer_count;
+    if ((PT_TRACE_STATS && (p.debug & 16)) && blockIdx.x == 0 && threadIdx.x == 0)
+        atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
+    for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
+        const int j = p.defer_slots[q];
+        const int src = slot_source(p, j);
+        const float4 a = p.ray[in_buf][0][src];
+        const float4 b = p.ray[in_buf][1][src];
+        const Hit h = intersect_scene<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
+                                                           s_stack + threadIdx.x, s_hs + threadIdx.x);
+        p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+        p.hitm[j] = h.model;
+    }
+}
+
 // One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
 template <bool FIRST, int ACCEL, int BS>
 __global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter, int bounce) {
@@ -1327,6 +1698,7 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
+        *p.defer_count = 0;        // and no deferred grid_fast rays
     }
 }
 
@@ -1462,6 +1834,11 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         // ACCEL_BVH only: for ACCEL_GRID_FAST the fused kernel measured faster than every
         // split variant tried
         split_trace = cfg.accel == ACCEL_BVH && !(e && std::atoi(e) == 0);
+        // ACCEL_GRID_FAST: persistent k_trace_gf (PT_GF_SPLIT=0 keeps the fused kernel)
+        const char* eg = std::getenv("PT_GF_SPLIT");
+        if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
+        const char* gff = std::getenv("PT_GF_FLAGS");
+        gf_flags = gff ? std::atoi(gff) : 9;
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
@@ -1478,8 +1855,13 @@ int Renderer::allocateOnGPU(const Scene& scene) {
             last_error = "BVH4 too deep for the traversal stack";
             return -1;
         }
-        kp.spill_stride = split_trace && (kp.trace_flags & 16) ? trace_blocks * 64 : 1;
+        const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (kp.trace_flags & 16));
+        kp.spill_stride = spills ? trace_blocks * 64 : 1;
         PT_HIP(upload(allocs, &kp.spill, nullptr, (size_t)kp.spill_stride * kSpillEntries * sizeof(int), stream));
+        const size_t dcap = split_trace && cfg.accel == ACCEL_GRID_FAST ? cap : 1;
+        PT_HIP(upload(allocs, &kp.defer_slots, nullptr, dcap * sizeof(int), stream));
+        PT_HIP(upload(allocs, &kp.defer_count, nullptr, sizeof(int), stream));
+        PT_HIP(hipMemsetAsync(kp.defer_count, 0, sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
         PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.trace_next, nullptr, sizeof(int), stream));
@@ -1516,6 +1898,16 @@ int Renderer::launchPrimary() {
 
 void Renderer::launchTrace(int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
+    if (cfg.accel == ACCEL_GRID_FAST) {
+        switch (gf_flags) {
+            case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, stream, kp, b); break;
+            case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, stream, kp, b); break;
+            case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b); break;
+            default: hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, stream, kp, b); break;
+        }
+        hipLaunchKernelGGL(k_trace_deferred<64>, g, t, 0, stream, kp, b);
+        return;
+    }
     switch (kp.trace_flags & 31) {
         case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, stream, kp, b); break;
         case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, stream, kp, b); break;

@@ -70,7 +70,7 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
-        allc = rs[v].segments_per_bounce(94)
+        allc = rs[v].segments_per_bounce(95)
         if allc[71]:
             it = allc[71]
             out[v]["trace_iters_per_wave_total"] = it
@@ -80,7 +80,19 @@ def main():
             out[v]["lanes_per_phase_iter"] = {k: round(b / max(a, 1), 2) for k, (a, b) in ph.items()}
             out[v]["select_loop_trips"] = allc[76]
             out[v]["deferred"] = allc[77]
-        if allc[84]:                                   # PT_TRACE_STATS build, PT_DEBUG_ABLATE & 4
+            sg = max(rs[v].segments(), 1)
+            out[v]["wave_iters_per_segment"] = round(it / sg, 3)
+            out[v]["phase_iters_per_segment"] = {k: round(a / sg, 3) for k, (a, b) in ph.items()}
+        if "PT_DEBUG_ABLATE=32" in v or "PT_DEBUG_ABLATE=96" in v:   # cycle stamps
+            cyc = allc[83:88]
+            tot = max(sum(cyc), 1)
+            out[v]["cycle_share"] = dict(zip(["refill", "select", "leaf", "node", "walk"], [round(c / tot, 3) for c in cyc]))
+            out[v]["wave_cycles_per_segment"] = round(tot / max(rs[v].segments(), 1), 1)
+        if "PT_DEBUG_ABLATE=96" in v:
+            w3 = allc[92:95]
+            out[v]["walk_wave_cycles_per_segment"] = dict(zip(["init_union", "skip", "steps"],
+                                                              [round(c / max(rs[v].segments(), 1), 1) for c in w3]))
+        elif allc[84]:                                 # PT_TRACE_STATS build, PT_DEBUG_ABLATE & 4
             segs_all = rs[v].segments()
             out[v]["walk_steps_per_walk"] = round(allc[83] / allc[84], 2)
             out[v]["walks_per_segment"] = round(allc[84] / segs_all, 3)

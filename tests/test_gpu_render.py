@@ -247,6 +247,10 @@ def test_grid_fast_hitset_overflow_falls_back_exactly(gpu, pt_mod, oracle_mod, a
     (1, {"PT_TRACE_FLAGS": "11", "PT_TRACE_WAVES_PER_CU": "1"}),
     (1, {"PT_TRACE_FLAGS": "27"}),
     (1, {"PT_TRACE_FLAGS": "19", "PT_BVH_LEAF": "16"}),
+    (2, {"PT_GF_SPLIT": "0"}),
+    (2, {"PT_GF_FLAGS": "0"}),
+    (2, {"PT_GF_FLAGS": "8", "PT_TRACE_REFILL": "1"}),
+    (2, {"PT_TRACE_WAVES_PER_CU": "1"}),
 ])
 def test_trace_kernel_variants_bitexact(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, env):
     """Every persistent-trace variant (fused / split, refill policy, phase
