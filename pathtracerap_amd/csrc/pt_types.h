@@ -24,7 +24,7 @@ enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2,
 enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1, ACCEL_GRID_FAST = 2 };
 
 // One instance (Model, Primitive.h:237-244) flattened for the kernels.
-// 58 dwords; read with wave-uniform (scalar) loads inside the model loop.
+// 66 dwords; read with wave-uniform (scalar) loads inside the model loop.
 struct ModelRec {
     float w2m[12];        // world_to_model columns 0..3, rows 0..2 (m[c*3+k])
     float m2w[12];        // model_to_world, same packing
@@ -41,8 +41,10 @@ struct ModelRec {
     float reach;          // R: max over triangles of the (tolerance-grown) voxel-box diameter, model units
     int bvh4_root;        // index of the mesh's 4-wide BLAS root node
     float wdelta;         // tier-1 window: the walk is exact up to t_min + wdelta
+    float ivw[3];         // 1 / vw (rounded; walk certificate only, used with margins)
+    float cslack[3];      // walk certificate: position slack per axis (DDA +EPSILON shift + rounding)
 };
-static_assert(sizeof(ModelRec) == 60 * 4, "ModelRec layout");
+static_assert(sizeof(ModelRec) == 66 * 4, "ModelRec layout");
 
 // 2-wide BVH node: both children's boxes in one 64-byte line.
 // link/count: count == 0 -> link is a child node index; count > 0 -> link is

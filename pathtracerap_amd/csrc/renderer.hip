@@ -31,6 +31,9 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP
 #define PT_HITCAP 6
 #endif
+#ifndef PT_WALK_CERT
+#define PT_WALK_CERT 1        // decide the common grid_fast walk from the ray's geometry (walk_certify)
+#endif
 #ifndef PT_WALK_SKIP
 #define PT_WALK_SKIP 1        // fast-forward the grid_fast walk to the members' union box (walk_skip)
 #endif
@@ -579,9 +582,86 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
     return walk_step_g<0>(p, d, [&](int h) { return hs[h * HSTRIDE]; }, nh, tmin, w);
 }
 
+// Walk certificate: decides from the ray's continuous geometry, without
+// stepping the DDA, the common case where the walk's first voxel inside the
+// members' union box U lies in the voxel box of the unique minimum-t member m*.
+// Before that voxel no voxel is a hit voxel (nothing outside U is), so the
+// walk cannot stop; in it m* is tested and the walk ends on its exact
+// "minimum-t member tested" shortcut with result (t_min, m*).  The entry voxel
+// is where the ray crosses U's face on the entering axis A; the other axes'
+// indices there are read off the ray's position, accepted only when that
+// position is farther from every voxel boundary than the DDA's own deviation
+// from the exact ray (its +EPSILON initial shift and the rounding of its
+// crossing parameters: ModelRec::cslack, plus the A-crossing's parameter error
+// times the slope).  Any doubt (zero slopes, ties at t_min, an entry at the
+// walk's start, a start within the shift of an interior boundary) -> false,
+// and the exact walk runs.
 template <int CAP, class GetM>
+__device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
+                                             GetM get, int nh, float tmin, float win, int& tri) {
+    int cnt = 0, blo = 0, bhi = 0, bi = -1;
+    int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 e = get(h);
+        if (__int_as_float(e.x) == tmin) { cnt++; blo = e.z; bhi = e.w; bi = e.y; }
+        ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
+        uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
+    }
+    if (cnt != 1 || d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) return false;
+    const float dd[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z}, pp[3] = {pt.x, pt.y, pt.z};
+    const int ul[3] = {ulx, uly, ulz}, uh[3] = {uhx, uhy, uhz};
+    float sin = -3.0e38f, sout = 3.0e38f;
+    int A = 0;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        // the walk's start index is the exact one unless pt lies within the shift of an interior boundary
+        const float q = (pp[a] - M.bbox[a]) * M.ivw[a];
+        const float n = rintf(q);
+        if (n >= 1.0f && n <= (float)(p.gdim[a] - 1) && absr(q - n) * M.vw[a] <= M.cslack[a]) return false;
+        const float lo = M.bbox[a] + (float)ul[a] * M.vw[a], hi = M.bbox[a] + (float)(uh[a] + 1) * M.vw[a];
+        const float s0 = (lo - pp[a]) * iv[a], s1 = (hi - pp[a]) * iv[a];
+        const float en = fminf(s0, s1), ex = fmaxf(s0, s1);
+        if (en > sin) { sin = en; A = a; }
+        sout = fminf(sout, ex);
+    }
+    const float span = M.vw[A] * (float)p.gdim[A];
+    const float err = 4.8e-7f * (float)(p.gdim[A] + 4) * (absr(sin) + 1.0f) +
+                      1e-6f * (absr(M.bbox[A]) + span + absr(pp[A])) * absr(iv[A]);
+    if (!(sin > 2.0f * err) || !(sout - sin > 2.0f * err)) return false;
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        int idx;
+        if (b == A) {
+            idx = dd[b] > 0.0f ? ul[b] : uh[b];
+        } else {
+            const float q = (pp[b] + dd[b] * sin - M.bbox[b]) * M.ivw[b];
+            const float f = floorf(q);
+            if (!(fminf(q - f, f + 1.0f - q) * M.vw[b] > M.cslack[b] + absr(dd[b]) * err)) return false;
+            idx = (int)f;
+        }
+        if (idx < ((blo >> (10 * b)) & 1023) || idx > ((bhi >> (10 * b)) & 1023)) return false;
+    }
+    if (!(t_box + sin + err < tmin + win)) return false;
+    tri = bi;
+    return true;
+}
+
+template <int CAP, class GetM, bool CERT = true>
 __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                                     GetM get, int nh, float tmin, float win) {
+#if PT_WALK_CERT
+    if (CERT) {
+        int tri;
+        if (walk_certify<CAP>(p, M, d, inv, pt, t_box, get, nh, tmin, win, tri)) {
+            if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 13 + kMaxBounceCounters, 1ull);
+            WalkResult r;
+            r.hit = true; r.t = tmin; r.tri = tri; r.has_best = true; r.final_min = true; r.tw = 0.0f;
+            return r;
+        }
+    }
+#endif
     const bool stamps = PT_TRACE_STATS && (p.debug & 64);     // wave cycles: init+union, skip, steps
     unsigned long long c0 = stamps ? clock64() : 0;
     Walk w;
@@ -631,14 +711,15 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
 
 // The same walk over at most CAP members copied to registers first: the walk's
 // per-voxel membership tests then wait on no LDS reads.
-template <int CAP, int HSTRIDE>
+template <int CAP, int HSTRIDE, bool CERT = true>
 __device__ __forceinline__ WalkResult hitset_walk_regs(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt,
                                                        float t_box, const int4* __restrict__ hs, int nh, float tmin,
                                                        float win) {
     int4 mem[CAP];
 #pragma unroll
     for (int h = 0; h < CAP; h++) mem[h] = h < nh ? hs[h * HSTRIDE] : make_int4(0, 0, 0, 0);
-    return hitset_walk_g<CAP>(p, M, d, inv, pt, t_box, [&](int h) { return mem[h]; }, nh, tmin, win);
+    auto get = [&](int h) { return mem[h]; };
+    return hitset_walk_g<CAP, decltype(get), CERT>(p, M, d, inv, pt, t_box, get, nh, tmin, win);
 }
 
 // Overflow tiers of grid_hitset: bounded, then unbounded collection into a
@@ -1273,6 +1354,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     float t_box = 0.0f, tmin = kFMax, margin = 0.0f;
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
+    int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // F & 4: the wave's claimed source block (uniform)
+    const int nb_prev = ((bounce == 1 ? p.npix : p.n_live[bounce - 1]) + p.chunk - 1) / p.chunk;
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
     bool exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
@@ -1281,9 +1364,38 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
     for (unsigned iters = 0;; iters++) {
-        const unsigned long long idle = __ballot(state == 0);
+        unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        if ((F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+            // claim whole source blocks of the previous bounce: block b's survivors sit at
+            // [b*CH, b*CH + cnt_b) and own dense slots [blk_off[b], blk_off[b] + cnt_b)
+            for (int guard = 0; guard < 4 && idle; guard++) {
+                if (q_pos >= q_cnt) {
+                    int b = 0;
+                    if (lane == 0) b = atomicAdd(p.trace_next, 1);
+                    b = __shfl(b, 0);
+                    if (b >= nb_prev) { exhausted = true; break; }
+                    q_b = b; q_pos = 0; q_cnt = p.blk_cnt[b]; q_off = p.blk_off[b];
+                    continue;
+                }
+                const int take = min(__popcll(idle), q_cnt - q_pos);
+                const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+                if (state == 0 && rank < take) {
+                    const int src = q_b * p.chunk + q_pos + rank;
+                    j = q_off + q_pos + rank;
+                    const float4 a = p.ray[in_buf][0][src];
+                    const float4 b = p.ray[in_buf][1][src];
+                    ow = mk3(a.x, a.y, a.z);
+                    dw = mk3(b.x, b.y, b.z);
+                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                    dlen = sqrtf(dot(dw, dw));
+                    gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
+                    state = 1;
+                }
+                q_pos += take;
+                idle = __ballot(state == 0);
+            }
+        } else if (!(F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
@@ -1481,7 +1593,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             // no accepted triangle anywhere on the ray (the first tier's bound is open
             // until the first member): no hit voxel, the model is missed
             state = nh == 0 ? 1 : 5;
-        } else if ((phase & 8) && state == 5) {          // the whole walk of the collected hit set
+        } else if ((phase & 8) && state == 5) {          // the walk: certificate, else the exact walk
             const ModelRec& M = models[im];
             const float win = tier == 0 ? M.wdelta : (tier == 1 ? 2.0f * M.reach : 3.0e38f);
             const f3 pt = o + d * t_box;
@@ -1903,6 +2015,7 @@ void Renderer::launchTrace(int b) {
             case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, stream, kp, b); break;
             case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, stream, kp, b); break;
             case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b); break;
+            case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, stream, kp, b); break;
             default: hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, stream, kp, b); break;
         }
         hipLaunchKernelGGL(k_trace_deferred<64>, g, t, 0, stream, kp, b);

@@ -632,6 +632,16 @@ void Scene::buildDeviceTables() {
         r.reach = std::isfinite(R) ? (float)R : 3e38f;
         const double W = 0.05 * vd + 1e-4 * bd + 1e-3;
         r.wdelta = std::isfinite(W) ? (float)W : 3e38f;
+        // Walk certificate (renderer.hip walk_certify): position slack that covers the
+        // DDA's +EPSILON initial-index shift and the rounding of its crossing
+        // parameters (<= 26 rounded adds of positive steps, plus the initial
+        // (boundary - pt) * inv) relative to the exact ray, per axis.
+        for (int k = 0; k < 3; k++) {
+            r.ivw[k] = (float)(1.0 / (double)g.voxel_width[k]);
+            const double span = (double)g.voxel_width[k] * grid_dim[k];
+            const double mag = std::fabs((double)r.bbox[k]) + std::fabs((double)r.bbox[k + 3]) + span;
+            r.cslack[k] = (float)(2.0 * kEps + 4.8e-7 * (grid_dim[k] + 4) * mag);
+        }
     }
 }
 

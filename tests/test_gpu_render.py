@@ -251,6 +251,8 @@ def test_grid_fast_hitset_overflow_falls_back_exactly(gpu, pt_mod, oracle_mod, a
     (2, {"PT_GF_FLAGS": "0"}),
     (2, {"PT_GF_FLAGS": "8", "PT_TRACE_REFILL": "1"}),
     (2, {"PT_TRACE_WAVES_PER_CU": "1"}),
+    (2, {"PT_GF_FLAGS": "13"}),
+    (2, {"PT_GF_FLAGS": "13", "PT_TRACE_REFILL": "1", "PT_TRACE_WAVES_PER_CU": "1"}),
 ])
 def test_trace_kernel_variants_bitexact(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, env):
     """Every persistent-trace variant (fused / split, refill policy, phase
@@ -302,3 +304,51 @@ def test_grid_fast_member_box_missed_far_hit(gpu, pt_mod, oracle_mod, accel):
     assert (ot > 50000).sum() >= 24                  # the reference returns the far triangle
     assert_bitexact(m, om, "model")
     assert_bitexact(t, ot, "dist")
+
+
+def _boundary_rays(a, n, seed):
+    """Rays whose origins and targets sit on, or within a few EPSILON of, voxel
+    boundaries of every model's grid (identity transforms: world == model
+    space), with some nearly axis-parallel directions."""
+    rs = np.random.RandomState(seed)
+    bb = a["mesh_bbox"].reshape(-1, 6).astype(np.float64)
+    vw = a["grid_vw"].reshape(-1, 3).astype(np.float64)
+    offs = np.array([0.0, 0.0025, -0.0025, 0.005, -0.005, 0.0099, -0.0099, 0.02, -0.02, 0.5, -0.5])
+    o = np.empty((n, 3)); tgt = np.empty((n, 3))
+    for i in range(n):
+        g = rs.randint(len(bb))
+        for arr in (o, tgt):
+            p = bb[g, :3] + rs.uniform(-0.1, 1.1, 3) * (bb[g, 3:] - bb[g, :3])
+            for k in range(3):
+                if rs.rand() < 0.6:
+                    j = rs.randint(0, 26)
+                    p[k] = bb[g, k] + j * vw[g, k] + offs[rs.randint(len(offs))]
+            arr[i] = p
+    d = tgt - o
+    m = rs.rand(n) < 0.3
+    ax = rs.randint(0, 3, n)
+    d[m, ax[m]] *= 10.0 ** rs.uniform(-7, -3, m.sum())
+    return o.astype(np.float32), d.astype(np.float32)
+
+
+def test_grid_fast_voxel_boundary_rays(gpu, pt_mod, oracle_mod):
+    """grid_fast == the reference grid on rays that start, pass and end on voxel
+    boundaries (the walk certificate's margins, the DDA's +EPSILON shift)."""
+    from pathtracerap_amd.synthetic import room_mesh, torus_mesh
+    P, O = pt_mod, oracle_mod
+    s = P.Scene()
+    t = s.addMesh(*torus_mesh(3000, seed=2))
+    rm = s.addMesh(*room_mesh())
+    s.addModel(t, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.addModel(rm, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.build(bvh=True)
+    a = s.export()
+    r = P.Renderer(P.RenderConfig(width=8, height=8, accel=2))
+    r.allocateOnGPU(s)
+    o, d = _boundary_rays(a, 60000, 5)
+    tt, nn, mm = r.intersect_rays(o, d)
+    r.free()
+    ot, on, om = O.intersect_rays(flat_from_export(a), o, d, accel=0)
+    assert (om >= 0).mean() > 0.3
+    assert_bitexact(mm, om, "model")
+    assert_bitexact(tt, ot, "dist")
