@@ -518,7 +518,10 @@ __device__ __forceinline__ void walk_skip(f3 d, Walk& w) {
 
 // One voxel of the walk; returns true when the walk has stopped.  Members
 // through `get`; CAP > 0: a register array of CAP entries (unrolled).
-template <int CAP, class GetM>
+// STRICT (the k_trace_gf collection, whose uncollected members may have any t):
+// only the minimum-t shortcut ends the walk early, and leaving the union box
+// after a hit voxel does not -- the walk steps on to the reference's own stop.
+template <int CAP, class GetM, bool STRICT = false>
 __device__ __forceinline__ bool walk_step_g(const KParams& p, f3 d, GetM get, int nh, float tmin, Walk& w) {
     const int ulx = w.ul & 1023, uly = (w.ul >> 10) & 1023, ulz = (w.ul >> 20) & 1023;
     const int uhx = w.uh & 1023, uhy = (w.uh >> 10) & 1023, uhz = (w.uh >> 20) & 1023;
@@ -546,9 +549,10 @@ __device__ __forceinline__ bool walk_step_g(const KParams& p, f3 d, GetM get, in
     // result and the return value are final; once the monotone walk has passed
     // the union box along an axis it enters no member's box again.
     const unsigned long long all = nh >= 64 ? ~0ull : ((1ull << nh) - 1ull);
-    if (w.tested == all || (w.bk >= 0 && w.bt == tmin)) return true;
+    if ((!STRICT && w.tested == all) || (w.bk >= 0 && w.bt == tmin)) return true;
     const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1, sz = d.z > 0.0f ? 1 : -1;
-    if ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz)) {
+    if ((!STRICT || !w.hit) &&
+        ((sx > 0 ? ix > uhx : ix < ulx) || (sy > 0 ? iy > uhy : iy < uly) || (sz > 0 ? iz > uhz : iz < ulz))) {
         w.passed = true;
         return true;
     }
@@ -648,7 +652,7 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
     return true;
 }
 
-template <int CAP, class GetM, bool CERT = true>
+template <int CAP, class GetM, bool CERT = true, bool STRICT = false>
 __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                                     GetM get, int nh, float tmin, float win) {
 #if PT_WALK_CERT
@@ -673,7 +677,7 @@ __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const Mode
 #endif
     unsigned long long c2 = stamps ? clock64() : 0;
     unsigned steps = 1;
-    while (!walk_step_g<CAP>(p, d, get, nh, tmin, w)) steps++;
+    while (!walk_step_g<CAP, GetM, STRICT>(p, d, get, nh, tmin, w)) steps++;
     if (stamps) {
         const unsigned long long c3 = clock64();
         if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
@@ -703,15 +707,16 @@ __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const Mode
     return r;
 }
 
-template <int HSTRIDE>
+template <int HSTRIDE, bool STRICT = false>
 __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                   const int4* __restrict__ hs, int nh, float tmin, float win) {
-    return hitset_walk_g<0>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * HSTRIDE]; }, nh, tmin, win);
+    auto get = [&](int h) { return hs[h * HSTRIDE]; };
+    return hitset_walk_g<0, decltype(get), true, STRICT>(p, M, d, inv, pt, t_box, get, nh, tmin, win);
 }
 
 // The same walk over at most CAP members copied to registers first: the walk's
 // per-voxel membership tests then wait on no LDS reads.
-template <int CAP, int HSTRIDE, bool CERT = true>
+template <int CAP, int HSTRIDE, bool CERT = true, bool STRICT = false>
 __device__ __forceinline__ WalkResult hitset_walk_regs(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt,
                                                        float t_box, const int4* __restrict__ hs, int nh, float tmin,
                                                        float win) {
@@ -719,7 +724,7 @@ __device__ __forceinline__ WalkResult hitset_walk_regs(const KParams& p, const M
 #pragma unroll
     for (int h = 0; h < CAP; h++) mem[h] = h < nh ? hs[h * HSTRIDE] : make_int4(0, 0, 0, 0);
     auto get = [&](int h) { return mem[h]; };
-    return hitset_walk_g<CAP, decltype(get), CERT>(p, M, d, inv, pt, t_box, get, nh, tmin, win);
+    return hitset_walk_g<CAP, decltype(get), CERT, STRICT>(p, M, d, inv, pt, t_box, get, nh, tmin, win);
 }
 
 // Overflow tiers of grid_hitset: bounded, then unbounded collection into a
@@ -1324,6 +1329,38 @@ __global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
 
+// Collection window of k_trace_gf, on voxel boxes instead of the reach R: the
+// walk can enter member h's voxel box before X = t_min + window only if the
+// exact ray enters that box grown by ModelRec::cslack (the DDA's deviation from
+// the ray) before X (+ a parameter slack).  A BLAS node can hold such a member
+// only if the ray enters its box grown by one voxel + cslack per axis before X
+// (a member's voxel box lies in the node box rounded out to voxels); that entry
+// is the node box's per-axis entries minus (vw + cslack) * |1/d| (the G terms).
+__device__ __forceinline__ float gf_slack(float x, float t_box) {
+    return 1e-5f * (absr(x) + absr(t_box) + 1.0f);
+}
+__device__ __forceinline__ float vbox_entry(const ModelRec& M, int lo, int hi, f3 o, f3 ninv) {
+    float tn = -3.0e38f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z), ia = a == 0 ? ninv.x : (a == 1 ? ninv.y : ninv.z);
+        const float l = M.bbox[a] + (float)((lo >> (10 * a)) & 1023) * M.vw[a] - M.cslack[a];
+        const float h = M.bbox[a] + (float)(((hi >> (10 * a)) & 1023) + 1) * M.vw[a] + M.cslack[a];
+        tn = fmaxf(tn, fminf((l - oa) * ia, (h - oa) * ia));
+    }
+    return tn;
+}
+__device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3 o, f3 inv, f3 G, float& tn, float& tf,
+                                            float& tnx) {
+    const float a0 = (lo[0] - o.x) * inv.x, b0 = (hi[0] - o.x) * inv.x;
+    const float a1 = (lo[1] - o.y) * inv.y, b1 = (hi[1] - o.y) * inv.y;
+    const float a2 = (lo[2] - o.z) * inv.z, b2 = (hi[2] - o.z) * inv.z;
+    const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
+    tn = fmaxf(fmaxf(e0, e1), e2);
+    tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
+    tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
+}
+
 template <int BS, int F>
 __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce) {
     __shared__ int s_stack[kGfStack * BS];
@@ -1350,8 +1387,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
     float dlen = 0.0f, gdist = kFMax;
     int gmodel = -1, gtri = -1, im = -1;
-    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), inv = mk3(0, 0, 0);
-    float t_box = 0.0f, tmin = kFMax, margin = 0.0f;
+    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0), G = mk3(0, 0, 0);
+    float t_box = 0.0f, tmin = kFMax, win = 0.0f;
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
     int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // F & 4: the wave's claimed source block (uniform)
@@ -1463,12 +1500,15 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
-                inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+                const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
                 const f3 pt = o + d * t_box;
                 if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
+                ninv = node_inv(inv);
+                G = mk3((M.vw[0] + M.cslack[0]) * absr(ninv.x), (M.vw[1] + M.cslack[1]) * absr(ninv.y),
+                        (M.vw[2] + M.cslack[2]) * absr(ninv.z));
                 tier = 0;
-                margin = M.wdelta + M.reach;
+                win = (PT_TRACE_STATS && (p.debug & 256)) ? 0.0f : M.wdelta;   // 256: timing-only ablation
                 cur = M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax; pblk = -1;
                 state = 2;
@@ -1482,7 +1522,10 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             float t;
             if (tri_test_rec(A, B, C, o, d, t)) {
                 if (t < tmin) tmin = t;
-                if (!(t > tmin + margin)) {             // required member (NaN is kept)
+                const ModelRec& M = models[im];
+                const float X = tmin + win;
+                const float Xs = X + gf_slack(X, t_box);
+                if (!(vbox_entry(M, __float_as_int(B.w), __float_as_int(C.w), o, ninv) > Xs)) {   // required member
                     const int4 e = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
                                              __float_as_int(C.w));
                     if (pblk < 0) {
@@ -1490,7 +1533,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                             int wn = 0;
                             for (int q = 0; q < nh; q++) {
                                 const int4 x = hs[q * BS];
-                                if (!(__int_as_float(x.x) > tmin + margin)) hs[(wn++) * BS] = x;
+                                if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) hs[(wn++) * BS] = x;
                             }
                             nh = wn;
                         }
@@ -1509,7 +1552,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                             int wn = 0;
                             for (int q = 0; q < nh; q++) {
                                 const int4 x = g[q];
-                                if (!(__int_as_float(x.x) > tmin + margin)) g[wn++] = x;
+                                if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) g[wn++] = x;
                             }
                             nh = wn;
                         }
@@ -1542,7 +1585,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                     }
                 }
             }
-        } else if ((phase & 2) && state == 2) {         // one node of the collection (bound t_min + margin)
+        } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
             const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
             const float4 q0 = nodes[4 * cur + 0];
             const float4 q1 = nodes[4 * cur + 1];
@@ -1552,13 +1595,13 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
             const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
             const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-            const f3 ninv = node_inv(inv);
-            float tn0, tf0, tn1, tf1;
-            node_slab(lo0, hi0, o, ninv, tn0, tf0);
-            node_slab(lo1, hi1, o, ninv, tn1, tf1);
-            const float bound = tmin + margin;
-            const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bound;
-            const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bound;
+            float tn0, tf0, tn1, tf1, tx0, tx1;
+            node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
+            node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
+            const float X = tmin + win;
+            const float bound = X + gf_slack(X, t_box);
+            const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tx0 <= bound;
+            const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tx1 <= bound;
             const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
             const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
             int next = -1;
@@ -1590,16 +1633,33 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         }
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
         if (collected) {
-            // no accepted triangle anywhere on the ray (the first tier's bound is open
-            // until the first member): no hit voxel, the model is missed
-            state = nh == 0 ? 1 : 5;
+            if (nh > 0) {
+                state = 5;
+            } else if (!(tmin < kFMax)) {
+                state = 1;          // no accepted triangle anywhere on the ray: no hit voxel, the model is missed
+            } else {
+                // accepted triangles exist, but none whose voxel box the walk can enter
+                // before t_min + window: the walk is not decided here, next tier
+                const ModelRec& M = models[im];
+                tier++;
+                win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
+                cur = M.bvh_root;
+                sp = 0; nh = 0; tmin = kFMax;
+                state = 2;
+            }
         } else if ((phase & 8) && state == 5) {          // the walk: certificate, else the exact walk
             const ModelRec& M = models[im];
-            const float win = tier == 0 ? M.wdelta : (tier == 1 ? 2.0f * M.reach : 3.0e38f);
             const f3 pt = o + d * t_box;
-            const WalkResult w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
-                                          : hitset_walk<1>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool,
-                                                           nh, tmin, win);
+            const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+            WalkResult w;
+            if (PT_TRACE_STATS && (p.debug & 128) && pblk < 0) {      // timing-only ablation: no walk at all
+                w.hit = true; w.has_best = true; w.final_min = true; w.t = tmin; w.tri = -1; w.tw = 0.0f;
+                for (int h = 0; h < nh; h++) if (__int_as_float(hs[h * BS].x) == tmin) w.tri = hs[h * BS].y;
+            } else {
+                w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
+                             : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
+                                                    tmin, win);
+            }
             if (tier == 2 || w.final_min || w.tw < tmin + win) {
                 if (w.hit && w.has_best) {
                     const float dd = model_hit_dist(M, o, d, w.t, ow);
@@ -1608,7 +1668,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 state = 1;
             } else {                                    // not provably exact: next tier's collection
                 tier++;
-                margin = tier == 1 ? 3.0f * M.reach : 3.0e38f;
+                win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
                 cur = M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
@@ -1656,7 +1716,7 @@ __global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
 
 // One bounce for every live ray: gather -> intersect -> shade -> compact / accumulate.
 template <bool FIRST, int ACCEL, int BS>
-__global__ __launch_bounds__(BS, PT_MINWAVES) void k_bounce(KParams p, int iter, int bounce) {
+__global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_MINWAVES) void k_bounce(KParams p, int iter, int bounce) {
     __shared__ int s_stack[(!FIRST && ACCEL != ACCEL_GRID && ACCEL != kAccelHitBuffer) ? kStack * BS : 1];
     __shared__ int4 s_hs[(!FIRST && ACCEL == ACCEL_GRID_FAST) ? kHitCap * BS : 1];
     __shared__ int s_wave[BS / 64];
