@@ -72,6 +72,7 @@ struct KParams {
 };
 
 constexpr int kMaxBounceCounters = 64;
+constexpr int kDiagCounters = 64;        // diagnostic counters after the per-bounce ones (PT_TRACE_STATS builds)
 
 struct KernelStats {
     double bounce_ms = 0, scan_ms = 0, primary_ms = 0, first_ms = 0, trace_ms = 0;

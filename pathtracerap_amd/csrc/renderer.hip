@@ -603,51 +603,75 @@ __device__ __forceinline__ bool walk_step(const KParams& p, f3 d, const int4* __
 template <int CAP, class GetM>
 __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                              GetM get, int nh, float tmin, float win, int& tri) {
-    int cnt = 0, blo = 0, bhi = 0, bi = -1;
+    int cnt = 0;
     int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
 #pragma unroll
     for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
         if (CAP > 0 && h >= nh) break;
         const int4 e = get(h);
-        if (__int_as_float(e.x) == tmin) { cnt++; blo = e.z; bhi = e.w; bi = e.y; }
+        if (__int_as_float(e.x) == tmin) cnt++;
         ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
         uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
     }
-    if (cnt != 1 || d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) return false;
+#define PT_CERT_FAIL(r) { if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 32 + (r) + kMaxBounceCounters, 1ull); return false; }
+    if (cnt == 0) PT_CERT_FAIL(0)
+    if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) PT_CERT_FAIL(1)
     const float dd[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z}, pp[3] = {pt.x, pt.y, pt.z};
     const int ul[3] = {ulx, uly, ulz}, uh[3] = {uhx, uhy, uhz};
     float sin = -3.0e38f, sout = 3.0e38f;
     int A = 0;
+    int v0[3];
+    bool in0 = true;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         // the walk's start index is the exact one unless pt lies within the shift of an interior boundary
         const float q = (pp[a] - M.bbox[a]) * M.ivw[a];
         const float n = rintf(q);
-        if (n >= 1.0f && n <= (float)(p.gdim[a] - 1) && absr(q - n) * M.vw[a] <= M.cslack[a]) return false;
+        if (n >= 1.0f && n <= (float)(p.gdim[a] - 1) && absr(q - n) * M.vw[a] <= M.cslack[a]) PT_CERT_FAIL(2)
+        v0[a] = min(max((int)floorf(q), 0), p.gdim[a] - 1);
+        in0 = in0 && v0[a] >= ul[a] && v0[a] <= uh[a];
         const float lo = M.bbox[a] + (float)ul[a] * M.vw[a], hi = M.bbox[a] + (float)(uh[a] + 1) * M.vw[a];
         const float s0 = (lo - pp[a]) * iv[a], s1 = (hi - pp[a]) * iv[a];
         const float en = fminf(s0, s1), ex = fmaxf(s0, s1);
         if (en > sin) { sin = en; A = a; }
         sout = fminf(sout, ex);
     }
-    const float span = M.vw[A] * (float)p.gdim[A];
-    const float err = 4.8e-7f * (float)(p.gdim[A] + 4) * (absr(sin) + 1.0f) +
-                      1e-6f * (absr(M.bbox[A]) + span + absr(pp[A])) * absr(iv[A]);
-    if (!(sin > 2.0f * err) || !(sout - sin > 2.0f * err)) return false;
+    int va[3];
+    float te;
+    if (in0) {                                   // the walk starts inside U: its first voxel is the entry
+        va[0] = v0[0]; va[1] = v0[1]; va[2] = v0[2];
+        te = 0.0f;
+    } else {
+        const float span = M.vw[A] * (float)p.gdim[A];
+        const float err = 4.8e-7f * (float)(p.gdim[A] + 4) * (absr(sin) + 1.0f) +
+                          1e-6f * (absr(M.bbox[A]) + span + absr(pp[A])) * absr(iv[A]);
+        if (!(sin > 2.0f * err)) PT_CERT_FAIL(3)
+        if (!(sout - sin > 2.0f * err)) PT_CERT_FAIL(4)
 #pragma unroll
-    for (int b = 0; b < 3; b++) {
-        int idx;
-        if (b == A) {
-            idx = dd[b] > 0.0f ? ul[b] : uh[b];
-        } else {
-            const float q = (pp[b] + dd[b] * sin - M.bbox[b]) * M.ivw[b];
-            const float f = floorf(q);
-            if (!(fminf(q - f, f + 1.0f - q) * M.vw[b] > M.cslack[b] + absr(dd[b]) * err)) return false;
-            idx = (int)f;
+        for (int b = 0; b < 3; b++) {
+            if (b == A) {
+                va[b] = dd[b] > 0.0f ? ul[b] : uh[b];
+            } else {
+                const float q = (pp[b] + dd[b] * sin - M.bbox[b]) * M.ivw[b];
+                const float f = floorf(q);
+                if (!(fminf(q - f, f + 1.0f - q) * M.vw[b] > M.cslack[b] + absr(dd[b]) * err)) PT_CERT_FAIL(5)
+                va[b] = (int)f;
+            }
         }
-        if (idx < ((blo >> (10 * b)) & 1023) || idx > ((bhi >> (10 * b)) & 1023)) return false;
+        te = sin + err;
     }
-    if (!(t_box + sin + err < tmin + win)) return false;
+    // the walk tests every member whose box holds the entry voxel there, in index
+    // order: the minimum-t member with the lowest index among them wins
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 e = get(h);
+        if (__int_as_float(e.x) == tmin && vbox_has(e.z, e.w, va[0], va[1], va[2]) && e.y < bi) bi = e.y;
+    }
+    if (bi == 0x7fffffff) PT_CERT_FAIL(6)
+    if (!(t_box + te < tmin + win)) PT_CERT_FAIL(7)
+#undef PT_CERT_FAIL
     tri = bi;
     return true;
 }
@@ -2040,8 +2064,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
 
         PT_HIP(hipMemsetAsync(kp.trace_next, 0, sizeof(int), stream));
     }
-    PT_HIP(upload(allocs, &kp.segments, nullptr, (32 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.segments, 0, (32 + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(upload(allocs, &kp.segments, nullptr, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
+    PT_HIP(hipMemsetAsync(kp.segments, 0, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
@@ -2236,11 +2260,11 @@ long long Renderer::segments() {
 
 int Renderer::segmentsPerBounce(long long* out, int n) {
     if (!allocated) { last_error = "not allocated"; return -1; }
-    unsigned long long v[32 + kMaxBounceCounters];
+    unsigned long long v[kDiagCounters + kMaxBounceCounters];
     PT_HIP(hipMemcpyAsync(v, kp.segments, sizeof v, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n && i < kMaxBounceCounters + 31; i++) out[i] = (long long)v[1 + i];
-    for (int i = kMaxBounceCounters + 31; i < n; i++) out[i] = 0;
+    for (int i = 0; i < n && i < kMaxBounceCounters + kDiagCounters - 1; i++) out[i] = (long long)v[1 + i];
+    for (int i = kMaxBounceCounters + kDiagCounters - 1; i < n; i++) out[i] = 0;
     return 0;
 }
 

@@ -70,7 +70,7 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
-        allc = rs[v].segments_per_bounce(95)
+        allc = rs[v].segments_per_bounce(127)
         if allc[71]:
             it = allc[71]
             out[v]["trace_iters_per_wave_total"] = it
@@ -101,6 +101,12 @@ def main():
         if allc[86]:
             out[v]["collect_nodes_per_collection"] = round(allc[85] / allc[86], 2)
             out[v]["collections_per_segment"] = round(allc[86] / rs[v].segments(), 3)
+        cf = allc[95:103]
+        if any(cf):
+            out[v]["cert_fail_per_segment"] = dict(zip(["ties", "zero_dir", "start_shift", "starts_in_U", "grazes_U",
+                                                        "margin", "not_in_Bstar", "window"],
+                                                       [round(c / max(rs[v].segments(), 1), 4) for c in cf]))
+            out[v]["cert_ok_per_segment"] = round(allc[76] / max(rs[v].segments(), 1), 4)
         diag = allc[64:67]
         if any(diag):
             out[v]["diag_tier2_t1overflow_fallback"] = diag
