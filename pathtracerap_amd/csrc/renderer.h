@@ -69,6 +69,8 @@ struct KParams {
     int trace_flags;                    // k_trace_bvh variant: 1 LDS model records, 2 leaf steps, 4 block claims
     int* defer_slots;                   // k_trace_gf: slots whose hit set overflowed LDS (k_trace_deferred)
     int* defer_count;                   // reset by k_scan
+    int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
+    int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
 };
 
 constexpr int kMaxBounceCounters = 64;

@@ -47,7 +47,7 @@ constexpr int kBlock = 256;
 #define PT_XCD_MAP 0      // 1: XCD-contiguous chunk mapping (measured 20% slower: off)
 #endif
 #ifndef PT_FMA_NODES
-#define PT_FMA_NODES 0    // 1: node slab tests as fma(lo, inv, -o*inv) (measured neutral: off)
+#define PT_FMA_NODES 1    // node slab tests as fma(lo, inv, -o*inv): +1-2 % in the persistent traces (0: sub + mul)
 #endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
@@ -977,6 +977,7 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
 // Dense slot j of bounce `bounce` -> its index in the ray pool written by the
 // previous bounce (block-local compaction + k_scan offsets).
 __device__ __forceinline__ int slot_source(const KParams& p, int j) {
+    if (p.use_slotmap) return p.slot_src[j];        // one load instead of the search below
     const int chunk = j / p.chunk;
     int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
     while (lo < hi) {
@@ -1050,12 +1051,15 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
     return n;
 }
 
+#ifndef PT_BVH_MINWAVES
+#define PT_BVH_MINWAVES 1     // waves per SIMD the k_trace_bvh register allocation must allow (5 spills 3 VGPRs, no faster)
+#endif
 constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
 
 // F (compile-time variant): 1 = model records in LDS, 2 = leaf triangles as
 // their own steps, 4 = claim source blocks (else: claim slots + search).
 template <int BS, int F>
-__global__ __launch_bounds__(BS) void k_trace_bvh(KParams p, int bounce) {
+__global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, int bounce) {
     __shared__ int s_stack[kStack * BS];
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
@@ -1376,9 +1380,16 @@ __device__ __forceinline__ float vbox_entry(const ModelRec& M, int lo, int hi, f
 }
 __device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3 o, f3 inv, f3 G, float& tn, float& tf,
                                             float& tnx) {
+#if PT_FMA_NODES
+    const f3 oi = o * inv;   // hoisted out of the traversal loop by the compiler
+    const float a0 = __builtin_fmaf(lo[0], inv.x, -oi.x), b0 = __builtin_fmaf(hi[0], inv.x, -oi.x);
+    const float a1 = __builtin_fmaf(lo[1], inv.y, -oi.y), b1 = __builtin_fmaf(hi[1], inv.y, -oi.y);
+    const float a2 = __builtin_fmaf(lo[2], inv.z, -oi.z), b2 = __builtin_fmaf(hi[2], inv.z, -oi.z);
+#else
     const float a0 = (lo[0] - o.x) * inv.x, b0 = (hi[0] - o.x) * inv.x;
     const float a1 = (lo[1] - o.y) * inv.y, b1 = (hi[1] - o.y) * inv.y;
     const float a2 = (lo[2] - o.z) * inv.z, b2 = (hi[2] - o.z) * inv.z;
+#endif
     const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
     tn = fmaxf(fmaxf(e0, e1), e2);
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
@@ -1776,12 +1787,17 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
             h.model = p.cache_model[j];
         } else {
             // dense slot j -> (source block b, rank) via the scan of the previous bounce
-            int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
+            int src;
+            if (p.use_slotmap) {
+                src = p.slot_src[j];
+            } else {
+                int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
+                }
+                src = lo * BS + (j - p.blk_off[lo]);
             }
-            const int src = lo * BS + (j - p.blk_off[lo]);
             const float4 a = p.ray[in_buf][0][src];
             const float4 b = p.ray[in_buf][1][src];
             const float4 c = p.ray[in_buf][2][src];
@@ -1896,6 +1912,17 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
         *p.defer_count = 0;        // and no deferred grid_fast rays
     }
+}
+
+// Slot map for bounce+1: dense slot blk_off[b] + r <- source index b * chunk + r
+// (block b's r-th survivor), so readers of slot j need one load, not a search.
+__global__ __launch_bounds__(256) void k_slotmap(KParams p, int bounce) {
+    const int n = bounce == 0 ? p.npix : p.n_live[bounce];
+    const int CH = p.chunk;
+    const int i = blockIdx.x * 256 + threadIdx.x;   // source index
+    if (i >= ((n + CH - 1) / CH) * CH) return;
+    const int b = i / CH, r = i - b * CH;
+    if (r < p.blk_cnt[b]) p.slot_src[p.blk_off[b] + r] = i;
 }
 
 __global__ void k_selftest_math(int n, const float* x, const float* y, float* out) {
@@ -2057,6 +2084,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const size_t dcap = split_trace && cfg.accel == ACCEL_GRID_FAST ? cap : 1;
         PT_HIP(upload(allocs, &kp.defer_slots, nullptr, dcap * sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.defer_count, nullptr, sizeof(int), stream));
+        const char* sm = std::getenv("PT_SLOTMAP");
+        kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
+        PT_HIP(upload(allocs, &kp.slot_src, nullptr, (kp.use_slotmap ? cap : 1) * sizeof(int), stream));
         PT_HIP(hipMemsetAsync(kp.defer_count, 0, sizeof(int), stream));
         PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
         PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
@@ -2194,6 +2224,10 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
             hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, stream, kp, b);
             PT_HIP(hipGetLastError());
+            if (kp.use_slotmap && b + 1 < passes) {
+                hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((kp.nblocks * kp.chunk + 255) / 256)), dim3(256), 0, stream, kp, b);
+                PT_HIP(hipGetLastError());
+            }
             if (profiling) { hipEventRecord(e1, stream); scan_events.push_back({e0, e1}); }
         }
     }
