@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2
 
 /* Primitive.h:213-222 Material::MaterialType */
 enum {
@@ -64,6 +64,8 @@ typedef struct pt_render_config {
     double plane_z;           /* image plane z (Renderer.cpp:543), default 900 */
     double plane_x0, plane_y0, plane_w, plane_h;  /* Renderer.cpp:538-542: -10,-4,20,16 */
     int block;                /* bounce-kernel workgroup = compaction chunk: 64 (default), 128 or 256 */
+    int pipelines;            /* iterations in flight on their own HIP streams, 1..4 (default 3); results
+                                 are identical for every value (contributions merge in iteration order) */
 } pt_render_config;
 
 int pt_abi_version(void);

@@ -57,6 +57,7 @@ class _Cfg(ctypes.Structure):
         ("tail_drop", ctypes.c_int), ("cam", ctypes.c_double * 3), ("plane_z", ctypes.c_double),
         ("plane_x0", ctypes.c_double), ("plane_y0", ctypes.c_double),
         ("plane_w", ctypes.c_double), ("plane_h", ctypes.c_double), ("block", ctypes.c_int),
+        ("pipelines", ctypes.c_int),
     ]
 
 
@@ -153,6 +154,7 @@ class RenderConfig:
     plane_w: float = 20.0
     plane_h: float = 16.0
     block: int = 64
+    pipelines: int = 3    # iterations in flight (own HIP streams); results identical for any value
 
     def c(self) -> _Cfg:
         c = _Cfg()
@@ -164,6 +166,7 @@ class RenderConfig:
         c.plane_z, c.plane_x0, c.plane_y0, c.plane_w, c.plane_h = (
             self.plane_z, self.plane_x0, self.plane_y0, self.plane_w, self.plane_h)
         c.block = self.block
+        c.pipelines = self.pipelines
         return c
 
 

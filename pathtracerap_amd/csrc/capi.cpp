@@ -27,6 +27,7 @@ void pt_default_config(pt_render_config* c) {
     c->plane_z = d.plane_z; c->plane_x0 = d.plane_x0; c->plane_y0 = d.plane_y0;
     c->plane_w = d.plane_w; c->plane_h = d.plane_h;
     c->block = d.block;
+    c->pipelines = d.pipelines;
 }
 
 static pt::RenderConfig to_cfg(const pt_render_config* c) {
@@ -38,6 +39,7 @@ static pt::RenderConfig to_cfg(const pt_render_config* c) {
     d.plane_z = c->plane_z; d.plane_x0 = c->plane_x0; d.plane_y0 = c->plane_y0;
     d.plane_w = c->plane_w; d.plane_h = c->plane_h;
     d.block = c->block;
+    d.pipelines = c->pipelines;
     return d;
 }
 

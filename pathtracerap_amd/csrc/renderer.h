@@ -24,6 +24,7 @@ struct RenderConfig {            // Config.h + generateRaysKernel constants, at 
     int grid[3] = {25, 25, 25};           // GRID_X/Y/Z
     int tail_drop = 0;                    // replicate ceil(n/32) launch truncation (Renderer.cpp:573)
     int block = 64;                       // bounce-kernel workgroup size = compaction chunk (64/128/256)
+    int pipelines = 3;                    // iterations in flight on their own HIP streams (1..kMaxPipes)
     double cam[3] = {0.0, 0.0, 920.0};    // Renderer.cpp:528
     double plane_z = 900.0;               // Renderer.cpp:543
     double plane_x0 = -10.0, plane_y0 = -4.0, plane_w = 20.0, plane_h = 16.0;  // Renderer.cpp:538-542
@@ -69,6 +70,7 @@ struct KParams {
     int trace_flags;                    // k_trace_bvh variant: 1 LDS model records, 2 leaf steps, 4 block claims
     int* defer_slots;                   // k_trace_gf: slots whose hit set overflowed LDS (k_trace_deferred)
     int* defer_count;                   // reset by k_scan
+    float* contrib;                     // pipelines > 1: this pipeline's per-iteration contributions (k_merge)
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
 };
@@ -108,13 +110,20 @@ public:
 
 private:
     int launchPrimary();
-    void launchTrace(int b);
-    void launchBounce(bool first, dim3 grid, int iter, int b, int accel);
+    void launchTrace(const KParams& k, hipStream_t st, int b);
+    void launchBounce(const KParams& k, hipStream_t st, bool first, dim3 grid, int iter, int b, int accel);
+    int allocPipe(KParams& k, size_t cap, hipStream_t st);
     int fail(hipError_t e, const char* what);
     void freeBuffers();
 
-    KParams kp{};
-    hipStream_t stream = nullptr;
+    KParams kp{};                    // pipeline 0 (and everything the pipelines share)
+    hipStream_t stream = nullptr;    // the caller's stream; pipeline 0 runs on it
+    static constexpr int kMaxPipes = 4;
+    int npipes = 1;
+    KParams pk[kMaxPipes]{};         // pipeline i's parameters (pk[0] == kp)
+    hipStream_t pstream[kMaxPipes]{};    // pstream[0] == stream; 1.. created here
+    hipEvent_t merge_ev[kMaxPipes]{};    // last k_merge recorded on each pipeline
+    hipEvent_t fork_ev = nullptr;
     bool own_stream = false;
     bool stream_set = false;
     bool allocated = false;

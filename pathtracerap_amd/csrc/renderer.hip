@@ -1055,6 +1055,7 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 #define PT_BVH_MINWAVES 1     // waves per SIMD the k_trace_bvh register allocation must allow (5 spills 3 VGPRs, no faster)
 #endif
 constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
+constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
 
 // F (compile-time variant): 1 = model records in LDS, 2 = leaf triangles as
 // their own steps, 4 = claim source blocks (else: claim slots + search).
@@ -1819,10 +1820,20 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
     if (active && !alive) {
         // gatherImageDataKernel (Renderer.cpp:481-496): pixel += 1.0f * sqrt(color).
         // Each pixel has exactly one ray per iteration: no atomics needed.
-        float* px = p.image + 3 * (size_t)r.pixel;
-        px[0] += 1.0f * sqrtf(r.c.x);
-        px[1] += 1.0f * sqrtf(r.c.y);
-        px[2] += 1.0f * sqrtf(r.c.z);
+        // With several pipelines in flight the value goes to the pipeline's
+        // per-iteration contribution buffer and k_merge adds the buffers to the
+        // image in iteration order: the same one add per pixel per iteration.
+        if (p.contrib) {
+            float* cp = p.contrib + 3 * (size_t)r.pixel;
+            cp[0] = 1.0f * sqrtf(r.c.x);
+            cp[1] = 1.0f * sqrtf(r.c.y);
+            cp[2] = 1.0f * sqrtf(r.c.z);
+        } else {
+            float* px = p.image + 3 * (size_t)r.pixel;
+            px[0] += 1.0f * sqrtf(r.c.x);
+            px[1] += 1.0f * sqrtf(r.c.y);
+            px[2] += 1.0f * sqrtf(r.c.z);
+        }
     }
     // Block-local stable compaction (ballot + wave prefix), order == slot order.
     const unsigned long long m = __ballot(alive);
@@ -1890,8 +1901,8 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         s_total = s_part[1023];
         p.blk_off[nb] = s_part[1023];
         p.n_live[bounce + 1] = s_part[1023];
-        p.segments[0] += (unsigned long long)n;
-        if (bounce < kMaxBounceCounters) p.segments[1 + bounce] += (unsigned long long)n;
+        atomicAdd(p.segments, (unsigned long long)n);           // shared by concurrent pipelines
+        if (bounce < kMaxBounceCounters) atomicAdd(p.segments + 1 + bounce, (unsigned long long)n);
     }
     __syncthreads();
     if (staged) {
@@ -1937,6 +1948,13 @@ __global__ void k_selftest_math(int n, const float* x, const float* y, float* ou
     out[5 * i + 4] = x[i] / y[i];
 }
 
+// image += contribution of one iteration: one add per element, n = W*H*3 floats
+// (scalar: the image may be a caller-bound buffer with only 4-byte alignment).
+__global__ __launch_bounds__(256) void k_merge(float* __restrict__ image, const float* __restrict__ contrib, size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) image[i] += contrib[i];
+}
+
 __global__ void k_zero(float* a, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) a[i] = 0.0f;
@@ -1974,7 +1992,10 @@ int Renderer::bindImage(float* device_rgb) {
     if (allocated && !external_image && kp.image) { last_error = "bind_image must precede allocateOnGPU"; return -1; }
     ext_image = device_rgb;
     external_image = device_rgb != nullptr;
-    if (allocated) kp.image = device_rgb;
+    if (allocated) {
+        kp.image = device_rgb;
+        for (int i = 0; i < kMaxPipes; i++) pk[i].image = device_rgb;
+    }
     return 0;
 }
 
@@ -2037,27 +2058,15 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     kp.plane_x0 = cfg.plane_x0;
     kp.plane_y0 = cfg.plane_y0;
     const size_t cap = (size_t)kp.nblocks * kp.chunk;
-    for (int b = 0; b < 2; b++)
-        for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &kp.ray[b][q], nullptr, cap * sizeof(float4), stream));
     PT_HIP(upload(allocs, &kp.cache_hit, nullptr, cap * sizeof(float4), stream));
     PT_HIP(upload(allocs, &kp.cache_model, nullptr, cap * sizeof(int), stream));
     if (external_image) kp.image = ext_image;
     else PT_HIP(upload(allocs, &kp.image, nullptr, (size_t)npix_all * 3 * sizeof(float), stream));
-    PT_HIP(upload(allocs, &kp.blk_cnt, nullptr, (kp.nblocks + 1) * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.blk_off, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.dst_start, nullptr, (kp.nblocks + 2) * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.n_live, nullptr, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
     kp.hs_pool_blocks = cfg.accel == ACCEL_GRID_FAST ? 65536 : 1;     // 64 MiB of 64-member blocks
-    PT_HIP(upload(allocs, &kp.hs_pool, nullptr, (size_t)kp.hs_pool_blocks * kHitCapPool * sizeof(int4), stream));
-    PT_HIP(upload(allocs, &kp.hs_pool_next, nullptr, sizeof(int), stream));
-    PT_HIP(hipMemsetAsync(kp.hs_pool_next, 0, sizeof(int), stream));
     {
-        // Persistent trace (ACCEL_BVH): hit buffer + work counter; PT_TRACE_SPLIT=0 keeps the fused kernel.
+        // Persistent trace + shading pass; PT_TRACE_SPLIT=0 / PT_GF_SPLIT=0 keep the fused kernel.
         const char* e = std::getenv("PT_TRACE_SPLIT");
-        // ACCEL_BVH only: for ACCEL_GRID_FAST the fused kernel measured faster than every
-        // split variant tried
         split_trace = cfg.accel == ACCEL_BVH && !(e && std::atoi(e) == 0);
-        // ACCEL_GRID_FAST: persistent k_trace_gf (PT_GF_SPLIT=0 keeps the fused kernel)
         const char* eg = std::getenv("PT_GF_SPLIT");
         if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
         const char* gff = std::getenv("PT_GF_FLAGS");
@@ -2071,36 +2080,71 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
         const int w = wpc ? std::max(1, std::atoi(wpc)) : 20;   // resident waves per CU
         trace_blocks = std::max(1, cus) * w;
-        const size_t hcap = split_trace ? cap : 1;
         // 4-wide traversal pushes up to 3 entries per level: LDS holds kStack, the rest spills
-        constexpr int kSpillEntries = 64;
         if (split_trace && (kp.trace_flags & 16) && 3 * scene.bvh4_max_depth > kStack + kSpillEntries) {
             last_error = "BVH4 too deep for the traversal stack";
             return -1;
         }
         const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (kp.trace_flags & 16));
         kp.spill_stride = spills ? trace_blocks * 64 : 1;
-        PT_HIP(upload(allocs, &kp.spill, nullptr, (size_t)kp.spill_stride * kSpillEntries * sizeof(int), stream));
-        const size_t dcap = split_trace && cfg.accel == ACCEL_GRID_FAST ? cap : 1;
-        PT_HIP(upload(allocs, &kp.defer_slots, nullptr, dcap * sizeof(int), stream));
-        PT_HIP(upload(allocs, &kp.defer_count, nullptr, sizeof(int), stream));
         const char* sm = std::getenv("PT_SLOTMAP");
         kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
-        PT_HIP(upload(allocs, &kp.slot_src, nullptr, (kp.use_slotmap ? cap : 1) * sizeof(int), stream));
-        PT_HIP(hipMemsetAsync(kp.defer_count, 0, sizeof(int), stream));
-        PT_HIP(upload(allocs, &kp.hit4, nullptr, hcap * sizeof(float4), stream));
-        PT_HIP(upload(allocs, &kp.hitm, nullptr, hcap * sizeof(int), stream));
-        PT_HIP(upload(allocs, &kp.trace_next, nullptr, sizeof(int), stream));
-
-        PT_HIP(hipMemsetAsync(kp.trace_next, 0, sizeof(int), stream));
     }
     PT_HIP(upload(allocs, &kp.segments, nullptr, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.segments, 0, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
-    PT_HIP(hipMemsetAsync(kp.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), stream));
+    // Pipelines: iterations in flight on their own streams, each with its own
+    // ray pools, scan state, hit buffer and work counters (PT_PIPES overrides).
+    {
+        const char* pe = std::getenv("PT_PIPES");
+        npipes = std::max(1, std::min(kMaxPipes, pe ? std::atoi(pe) : cfg.pipelines));
+    }
+    kp.contrib = nullptr;
+    pstream[0] = stream;
+    for (int i = 1; i < npipes; i++) {
+        if (!pstream[i]) PT_HIP(hipStreamCreateWithFlags(&pstream[i], hipStreamNonBlocking));
+    }
+    for (int i = 0; i < npipes; i++) {
+        pk[i] = kp;
+        if (allocPipe(pk[i], cap, stream) != 0) return -1;
+        if (npipes > 1) {
+            PT_HIP(upload(allocs, &pk[i].contrib, nullptr, (size_t)npix_all * 3 * sizeof(float), stream));
+            PT_HIP(hipMemsetAsync(pk[i].contrib, 0, (size_t)npix_all * 3 * sizeof(float), stream));
+        }
+        if (!merge_ev[i]) PT_HIP(hipEventCreateWithFlags(&merge_ev[i], hipEventDisableTiming));
+    }
+    if (!fork_ev) PT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    kp = pk[0];
     PT_HIP(hipStreamSynchronize(stream));
     allocated = true;
     cache_valid = false;
     return clearImage();
+}
+
+// One pipeline's buffers: ray pools, scan state, overflow pool, traversal
+// spill, hit buffer and work counters.
+int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
+    for (int b = 0; b < 2; b++)
+        for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &k.ray[b][q], nullptr, cap * sizeof(float4), st));
+    PT_HIP(upload(allocs, &k.blk_cnt, nullptr, (k.nblocks + 1) * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.blk_off, nullptr, (k.nblocks + 2) * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.dst_start, nullptr, (k.nblocks + 2) * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.n_live, nullptr, (size_t)(cfg.max_bounces + 4) * sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.n_live, 0, (size_t)(cfg.max_bounces + 4) * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.hs_pool, nullptr, (size_t)k.hs_pool_blocks * kHitCapPool * sizeof(int4), st));
+    PT_HIP(upload(allocs, &k.hs_pool_next, nullptr, sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.hs_pool_next, 0, sizeof(int), st));
+    PT_HIP(upload(allocs, &k.spill, nullptr, (size_t)k.spill_stride * kSpillEntries * sizeof(int), st));
+    const size_t dcap = split_trace && cfg.accel == ACCEL_GRID_FAST ? cap : 1;
+    PT_HIP(upload(allocs, &k.defer_slots, nullptr, dcap * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.defer_count, nullptr, sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.defer_count, 0, sizeof(int), st));
+    PT_HIP(upload(allocs, &k.slot_src, nullptr, (k.use_slotmap ? cap : 1) * sizeof(int), st));
+    const size_t hcap = split_trace ? cap : 1;
+    PT_HIP(upload(allocs, &k.hit4, nullptr, hcap * sizeof(float4), st));
+    PT_HIP(upload(allocs, &k.hitm, nullptr, hcap * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.trace_next, nullptr, sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.trace_next, 0, sizeof(int), st));
+    return 0;
 }
 
 int Renderer::clearImage() {
@@ -2122,32 +2166,32 @@ int Renderer::launchPrimary() {
     return 0;
 }
 
-void Renderer::launchTrace(int b) {
+void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
         switch (gf_flags) {
-            case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, stream, kp, b); break;
-            case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, stream, kp, b); break;
-            case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, stream, kp, b); break;
-            case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, stream, kp, b); break;
-            default: hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, stream, kp, b); break;
+            case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b); break;
+            case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b); break;
+            case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b); break;
+            case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b); break;
+            default: hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b); break;
         }
-        hipLaunchKernelGGL(k_trace_deferred<64>, g, t, 0, stream, kp, b);
+        hipLaunchKernelGGL(k_trace_deferred<64>, g, t, 0, st, k, b);
         return;
     }
-    switch (kp.trace_flags & 31) {
-        case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, stream, kp, b); break;
-        case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, stream, kp, b); break;
-        case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, stream, kp, b); break;
-        case 3: hipLaunchKernelGGL((k_trace_bvh<64, 3>), g, t, 0, stream, kp, b); break;
-        case 4: hipLaunchKernelGGL((k_trace_bvh<64, 4>), g, t, 0, stream, kp, b); break;
-        case 5: hipLaunchKernelGGL((k_trace_bvh<64, 5>), g, t, 0, stream, kp, b); break;
-        case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, stream, kp, b); break;
-        case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, stream, kp, b); break;
-        case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, stream, kp, b); break;
-        case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, stream, kp, b); break;
-        case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, stream, kp, b); break;
-        default: hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, stream, kp, b); break;
+    switch (k.trace_flags & 31) {
+        case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, st, k, b); break;
+        case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, st, k, b); break;
+        case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, st, k, b); break;
+        case 3: hipLaunchKernelGGL((k_trace_bvh<64, 3>), g, t, 0, st, k, b); break;
+        case 4: hipLaunchKernelGGL((k_trace_bvh<64, 4>), g, t, 0, st, k, b); break;
+        case 5: hipLaunchKernelGGL((k_trace_bvh<64, 5>), g, t, 0, st, k, b); break;
+        case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, st, k, b); break;
+        case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, st, k, b); break;
+        case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b); break;
+        case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, st, k, b); break;
+        case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, st, k, b); break;
+        default: hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b); break;
     }
 }
 
@@ -2161,19 +2205,19 @@ static void launch_bounce_bs(int accel, dim3 grid, hipStream_t st, const KParams
     else hipLaunchKernelGGL((k_bounce<FIRST, ACCEL_GRID, BS>), grid, dim3(BS), 0, st, kp, iter, b);
 }
 
-void Renderer::launchBounce(bool first, dim3 grid, int iter, int b, int accel) {
-    switch (kp.chunk) {
+void Renderer::launchBounce(const KParams& k, hipStream_t st, bool first, dim3 grid, int iter, int b, int accel) {
+    switch (k.chunk) {
         case 64:
-            if (first) launch_bounce_bs<true, 64>(accel, grid, stream, kp, iter, b);
-            else launch_bounce_bs<false, 64>(accel, grid, stream, kp, iter, b);
+            if (first) launch_bounce_bs<true, 64>(accel, grid, st, k, iter, b);
+            else launch_bounce_bs<false, 64>(accel, grid, st, k, iter, b);
             break;
         case 128:
-            if (first) launch_bounce_bs<true, 128>(accel, grid, stream, kp, iter, b);
-            else launch_bounce_bs<false, 128>(accel, grid, stream, kp, iter, b);
+            if (first) launch_bounce_bs<true, 128>(accel, grid, st, k, iter, b);
+            else launch_bounce_bs<false, 128>(accel, grid, st, k, iter, b);
             break;
         default:
-            if (first) launch_bounce_bs<true, 256>(accel, grid, stream, kp, iter, b);
-            else launch_bounce_bs<false, 256>(accel, grid, stream, kp, iter, b);
+            if (first) launch_bounce_bs<true, 256>(accel, grid, st, k, iter, b);
+            else launch_bounce_bs<false, 256>(accel, grid, st, k, iter, b);
             break;
     }
 }
@@ -2198,37 +2242,64 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
     }
     const dim3 grid((unsigned)kp.nblocks + 8u);
     const int passes = cfg.max_bounces > 1 ? cfg.max_bounces : 1;
+    const int np = npipes;
+    if (np > 1) {                                   // fork the pipeline streams off the caller's stream
+        PT_HIP(hipEventRecord(fork_ev, stream));
+        for (int q = 1; q < np; q++) PT_HIP(hipStreamWaitEvent(pstream[q], fork_ev, 0));
+    }
+    const size_t n3 = (size_t)cfg.width * cfg.height * 3;
     for (int it = 0; it < n_iters; it++) {
         const int iter = first_iter + it;
+        const int q = it % np;
+        const KParams& k = pk[q];
+        hipStream_t st = q == 0 ? stream : pstream[q];
         for (int b = 0; b < passes; b++) {
             hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
+            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             if (b > 0 && split_trace) {
-                launchTrace(b);
+                launchTrace(k, st, b);
                 PT_HIP(hipGetLastError());
                 if (profiling) {
-                    hipEventRecord(e1, stream);
+                    hipEventRecord(e1, st);
                     trace_events.push_back({e0, e1});
-                    hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream);
+                    hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st);
                 }
-                launchBounce(false, grid, iter, b, kAccelHitBuffer);
+                launchBounce(k, st, false, grid, iter, b, kAccelHitBuffer);
             } else {
-                launchBounce(b == 0, grid, iter, b, cfg.accel);
+                launchBounce(k, st, b == 0, grid, iter, b, cfg.accel);
             }
             PT_HIP(hipGetLastError());
             if (profiling) {
-                hipEventRecord(e1, stream);
+                hipEventRecord(e1, st);
                 (b == 0 ? first_events : bounce_events).push_back({e0, e1});
                 e0 = e1 = nullptr;
             }
-            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
-            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, stream, kp, b);
+            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, k, b);
             PT_HIP(hipGetLastError());
-            if (kp.use_slotmap && b + 1 < passes) {
-                hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((kp.nblocks * kp.chunk + 255) / 256)), dim3(256), 0, stream, kp, b);
+            if (k.use_slotmap && b + 1 < passes) {
+                hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((k.nblocks * k.chunk + 255) / 256)), dim3(256), 0, st, k, b);
                 PT_HIP(hipGetLastError());
             }
-            if (profiling) { hipEventRecord(e1, stream); scan_events.push_back({e0, e1}); }
+            if (profiling) { hipEventRecord(e1, st); scan_events.push_back({e0, e1}); }
+        }
+        if (np > 1) {
+            // image += this iteration's contributions, after the previous iteration's merge
+            if (it > 0) PT_HIP(hipStreamWaitEvent(st, merge_ev[(it - 1) % np], 0));
+            hipLaunchKernelGGL(k_merge, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, st, k.image, k.contrib, n3);
+            PT_HIP(hipGetLastError());
+            PT_HIP(hipEventRecord(merge_ev[q], st));
+        }
+    }
+    if (np > 1 && n_iters > 0) {                    // join: the last merge follows every earlier one
+        PT_HIP(hipStreamWaitEvent(stream, merge_ev[(n_iters - 1) % np], 0));
+        for (int q2 = 1; q2 < np; q2++) {           // and every pipeline's work has been merged
+            PT_HIP(hipStreamWaitEvent(stream, merge_ev[q2], 0));
+        }
+    } else if (np > 1) {
+        for (int q2 = 1; q2 < np; q2++) {           // nothing launched: still join the forked streams
+            PT_HIP(hipEventRecord(merge_ev[q2], pstream[q2]));
+            PT_HIP(hipStreamWaitEvent(stream, merge_ev[q2], 0));
         }
     }
     return 0;
@@ -2399,6 +2470,8 @@ int selftest_math(int n, const float* x, const float* y, float* out, std::string
 
 void Renderer::freeBuffers() {
     if (allocated || stream) hipStreamSynchronize(stream);
+    for (int i = 1; i < kMaxPipes; i++)
+        if (pstream[i]) hipStreamSynchronize(pstream[i]);
     for (void* p : allocs) hipFree(p);
     allocs.clear();
     kp.image = nullptr;
@@ -2416,6 +2489,16 @@ void Renderer::free() {
     bounce_events.clear();
     first_events.clear();
     scan_events.clear();
+    for (int i = 1; i < kMaxPipes; i++) {
+        if (pstream[i]) hipStreamDestroy(pstream[i]);
+        pstream[i] = nullptr;
+    }
+    for (int i = 0; i < kMaxPipes; i++) {
+        if (merge_ev[i]) hipEventDestroy(merge_ev[i]);
+        merge_ev[i] = nullptr;
+    }
+    if (fork_ev) hipEventDestroy(fork_ev);
+    fork_ev = nullptr;
     if (own_stream && stream) hipStreamDestroy(stream);
     stream = nullptr;
     own_stream = false;

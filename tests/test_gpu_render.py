@@ -352,3 +352,25 @@ def test_grid_fast_voxel_boundary_rays(gpu, pt_mod, oracle_mod):
     assert (om >= 0).mean() > 0.3
     assert_bitexact(mm, om, "model")
     assert_bitexact(tt, ot, "dist")
+
+
+@pytest.mark.parametrize("accel", [1, 2])
+def test_pipelines_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, accel):
+    """1..4 iterations in flight (own streams, contribution buffers merged in
+    iteration order) give the oracle's image bit for bit, incl. odd counts."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=3000, seed=5))
+    s.build(bvh=True)
+    want = None
+    for pipes in (1, 2, 3, 4):
+        cfg = P.RenderConfig(width=72, height=56, iterations=5, max_bounces=6, accel=accel, pipelines=pipes)
+        r = P.Renderer(cfg)
+        r.allocateOnGPU(s)
+        r.renderLoop(0, 2)
+        r.renderLoop(2, 3)                  # two calls: the join / fork across calls
+        img = r.image()
+        r.free()
+        if want is None:
+            want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg))
+        assert_bitexact(img, want, f"pipelines={pipes}")
