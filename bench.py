@@ -54,7 +54,12 @@ def parse():
     ap.add_argument("--metallic", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    ap.add_argument("--pipelines", type=int, default=0,
+                    help="iterations in flight on their own HIP streams (0: the library default)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4): one hardware queue per "
+                         "pipeline stream so iterations in flight do not serialise on a shared queue (max 32)")
     return ap.parse_args()
 
 
@@ -125,6 +130,8 @@ def load_pmc(kernel, workload_key):
 
 def main():
     args = parse()
+    if args.hw_queues > 0:     # read once by the HIP runtime at initialisation: set before torch touches it
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     import torch
     import torch.distributed as dist
 
@@ -147,6 +154,8 @@ def main():
     scene = P.Scene(scene_path)
     cfg = scene.apply_settings(P.RenderConfig())
     cfg.width, cfg.height, cfg.max_bounces, cfg.accel = args.width, args.height, args.bounces, accel
+    if args.pipelines > 0:
+        cfg.pipelines = args.pipelines
     scene.build(grid=cfg.grid, bvh=accel != P.ACCEL_GRID)
     ntri = scene.counts()["nt"]
 
@@ -163,9 +172,6 @@ def main():
     r.clearImage()
     seg0 = r.segments()
     pb0 = r.segments_per_bounce()
-    if not args.no_profile:
-        r.kernel_stats()          # reset
-        r.set_profiling(True)
 
     if world > 1:
         dist.barrier()
@@ -179,7 +185,6 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
 
-    stats = r.kernel_stats() if not args.no_profile else None
     seg = r.segments() - seg0
     per_bounce = [a - b for a, b in zip(r.segments_per_bounce(), pb0)]
     while per_bounce and per_bounce[-1] == 0:
@@ -194,13 +199,34 @@ def main():
     else:
         seg_total = float(seg)
     img_ok = bool(torch.isfinite(image).all().item())
+    pipes = r.pipelines()
     r.free()
+
+    # Per-kernel durations for the roofline come from a separate pass of the
+    # same K iterations with ONE pipeline: with several iterations in flight
+    # the kernels of different pipelines overlap and an event pair around one
+    # launch would also time its neighbours.  Same iteration ids => the same
+    # per-bounce ray counts as the timed pass.
+    stats = None
+    if not args.no_profile and rank == 0:
+        cfg_p = P.RenderConfig(**{**cfg.__dict__, "pipelines": 1})
+        rp = P.Renderer(cfg_p)
+        rp.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        rp.bind_image(image.data_ptr(), keepalive=image)
+        rp.allocateOnGPU(scene)
+        rp.renderLoop(first_iter=1_000_000, n_iters=W, sync=False)
+        torch.cuda.synchronize(dev)
+        rp.kernel_stats()          # reset
+        rp.set_profiling(True)
+        rp.renderLoop(first_iter=rank * K, n_iters=K, sync=True)
+        stats = rp.kernel_stats()
+        rp.free()
 
     alt = None
     if args.alt_accel and args.alt_accel != args.accel:
         acc2 = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[args.alt_accel]
         cfg2 = P.RenderConfig(width=cfg.width, height=cfg.height, max_bounces=cfg.max_bounces, accel=acc2,
-                              grid=cfg.grid, block=cfg.block)
+                              grid=cfg.grid, block=cfg.block, pipelines=cfg.pipelines)
         if acc2 != P.ACCEL_GRID and accel == P.ACCEL_GRID:
             scene.build(grid=cfg.grid, bvh=True)
         r2 = P.Renderer(cfg2)
@@ -289,7 +315,7 @@ def main():
                        "spp_per_step": 1, "accel": args.accel,
                        "results": "bit-identical to the reference algorithm (oracle-checked)"
                        if args.accel != "bvh" else "exact closest hit",
-                       "parallelism": f"samples sharded x{world}",
+                       "parallelism": f"samples sharded x{world}", "pipelines": pipes,
                        "segments": int(seg_total), "segments_per_bounce_rank0": per_bounce,
                        "image_finite": img_ok},
             "roofline": roof, "cpu_baseline": cpu, "alt_mode": alt,

@@ -64,7 +64,7 @@ typedef struct pt_render_config {
     double plane_z;           /* image plane z (Renderer.cpp:543), default 900 */
     double plane_x0, plane_y0, plane_w, plane_h;  /* Renderer.cpp:538-542: -10,-4,20,16 */
     int block;                /* bounce-kernel workgroup = compaction chunk: 64 (default), 128 or 256 */
-    int pipelines;            /* iterations in flight on their own HIP streams, 1..4 (default 3); results
+    int pipelines;            /* iterations in flight on their own HIP streams, 1..16 (default 8); results
                                  are identical for every value (contributions merge in iteration order) */
 } pt_render_config;
 
@@ -122,6 +122,8 @@ long long pt_renderer_segments(pt_renderer *r);
 /* out[b] = live rays entering bounce b, summed over the iterations rendered (b < n, n <= 64 useful). */
 int pt_renderer_segments_per_bounce(pt_renderer *r, long long *out, int n);
 int pt_renderer_set_profiling(pt_renderer *r, int on);
+/* Iterations in flight after allocate_on_gpu (config.pipelines clamped to 1..16, PT_PIPES overrides). */
+int pt_renderer_pipelines(pt_renderer *r);
 /* stats[0..6] = secondary-bounce ms, scan ms, primary ms, secondary-bounce launches,
  * scan launches, first-bounce ms, first-bounce launches (HIP events; resets). */
 int pt_renderer_kernel_stats(pt_renderer *r, double stats[7]);

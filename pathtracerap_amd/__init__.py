@@ -94,6 +94,7 @@ EXPORTS = [
     ("pt_renderer_render_image", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     ("pt_renderer_segments", ctypes.c_longlong, [ctypes.c_void_p]),
     ("pt_renderer_segments_per_bounce", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
+    ("pt_renderer_pipelines", ctypes.c_int, [ctypes.c_void_p]),
     ("pt_renderer_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("pt_renderer_kernel_stats", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     ("pt_renderer_kernel_stats_ex", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
@@ -154,7 +155,7 @@ class RenderConfig:
     plane_w: float = 20.0
     plane_h: float = 16.0
     block: int = 64
-    pipelines: int = 3    # iterations in flight (own HIP streams); results identical for any value
+    pipelines: int = 8    # iterations in flight (own HIP streams); results identical for any value
 
     def c(self) -> _Cfg:
         c = _Cfg()
@@ -323,6 +324,10 @@ class Renderer:
         out = (ctypes.c_longlong * n)()
         _err(lib().pt_renderer_segments_per_bounce(self._h, out, n), "segments_per_bounce")
         return list(out)
+
+    def pipelines(self) -> int:
+        """Iterations in flight (own HIP streams) once allocated."""
+        return _err(lib().pt_renderer_pipelines(self._h), "pipelines")
 
     def set_profiling(self, on: bool) -> None:
         _err(lib().pt_renderer_set_profiling(self._h, 1 if on else 0), "set_profiling")

@@ -219,6 +219,10 @@ int pt_renderer_segments_per_bounce(pt_renderer* r, long long* out, int n) {
     if (!out || n < 0) return set_err("bad arguments");
     R_CALL(r->r->segmentsPerBounce(out, n));
 }
+int pt_renderer_pipelines(pt_renderer* r) {
+    if (!r || !r->r) return set_err("null renderer");
+    return r->r->pipelines();
+}
 int pt_renderer_set_profiling(pt_renderer* r, int on) { R_CALL(r->r->setProfiling(on != 0)); }
 int pt_renderer_kernel_stats(pt_renderer* r, double st[7]) {
     if (!r || !r->r || !st) return set_err("null argument");

@@ -24,7 +24,7 @@ struct RenderConfig {            // Config.h + generateRaysKernel constants, at 
     int grid[3] = {25, 25, 25};           // GRID_X/Y/Z
     int tail_drop = 0;                    // replicate ceil(n/32) launch truncation (Renderer.cpp:573)
     int block = 64;                       // bounce-kernel workgroup size = compaction chunk (64/128/256)
-    int pipelines = 3;                    // iterations in flight on their own HIP streams (1..kMaxPipes)
+    int pipelines = 8;                    // iterations in flight on their own HIP streams (1..kMaxPipes)
     double cam[3] = {0.0, 0.0, 920.0};    // Renderer.cpp:528
     double plane_z = 900.0;               // Renderer.cpp:543
     double plane_x0 = -10.0, plane_y0 = -4.0, plane_w = 20.0, plane_h = 16.0;  // Renderer.cpp:538-542
@@ -101,6 +101,7 @@ public:
     int setProfiling(bool on);
     int kernelStats(KernelStats* out);
     long long segments();
+    int pipelines() const { return npipes; }
     int segmentsPerBounce(long long* out, int n);
     int primaryHits(float* dist, float* normal, int* model);
     int intersectRays(int n, const float* orig, const float* dir, float* dist, float* normal, int* model);
@@ -118,7 +119,7 @@ private:
 
     KParams kp{};                    // pipeline 0 (and everything the pipelines share)
     hipStream_t stream = nullptr;    // the caller's stream; pipeline 0 runs on it
-    static constexpr int kMaxPipes = 4;
+    static constexpr int kMaxPipes = 16;
     int npipes = 1;
     KParams pk[kMaxPipes]{};         // pipeline i's parameters (pk[0] == kp)
     hipStream_t pstream[kMaxPipes]{};    // pstream[0] == stream; 1.. created here

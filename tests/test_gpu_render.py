@@ -356,14 +356,14 @@ def test_grid_fast_voxel_boundary_rays(gpu, pt_mod, oracle_mod):
 
 @pytest.mark.parametrize("accel", [1, 2])
 def test_pipelines_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, accel):
-    """1..4 iterations in flight (own streams, contribution buffers merged in
+    """1..16 iterations in flight (own streams, contribution buffers merged in
     iteration order) give the oracle's image bit for bit, incl. odd counts."""
     from pathtracerap_amd import synthetic
     P, O = pt_mod, oracle_mod
     s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=3000, seed=5))
     s.build(bvh=True)
     want = None
-    for pipes in (1, 2, 3, 4):
+    for pipes in (1, 2, 3, 4, 8, 16):
         cfg = P.RenderConfig(width=72, height=56, iterations=5, max_bounces=6, accel=accel, pipelines=pipes)
         r = P.Renderer(cfg)
         r.allocateOnGPU(s)
