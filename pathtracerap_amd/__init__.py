@@ -57,7 +57,7 @@ class _Cfg(ctypes.Structure):
         ("tail_drop", ctypes.c_int), ("cam", ctypes.c_double * 3), ("plane_z", ctypes.c_double),
         ("plane_x0", ctypes.c_double), ("plane_y0", ctypes.c_double),
         ("plane_w", ctypes.c_double), ("plane_h", ctypes.c_double), ("block", ctypes.c_int),
-        ("pipelines", ctypes.c_int),
+        ("pipelines", ctypes.c_int), ("ray_sort", ctypes.c_int),
     ]
 
 
@@ -156,6 +156,7 @@ class RenderConfig:
     plane_h: float = 16.0
     block: int = 64
     pipelines: int = 8    # iterations in flight (own HIP streams); results identical for any value
+    ray_sort: int = -1    # ray sort key before each persistent trace (-1 auto, 0 off); results identical
 
     def c(self) -> _Cfg:
         c = _Cfg()
@@ -168,6 +169,7 @@ class RenderConfig:
             self.plane_z, self.plane_x0, self.plane_y0, self.plane_w, self.plane_h)
         c.block = self.block
         c.pipelines = self.pipelines
+        c.ray_sort = self.ray_sort
         return c
 
 

@@ -28,6 +28,7 @@ void pt_default_config(pt_render_config* c) {
     c->plane_w = d.plane_w; c->plane_h = d.plane_h;
     c->block = d.block;
     c->pipelines = d.pipelines;
+    c->ray_sort = d.ray_sort;
 }
 
 static pt::RenderConfig to_cfg(const pt_render_config* c) {
@@ -40,6 +41,7 @@ static pt::RenderConfig to_cfg(const pt_render_config* c) {
     d.plane_w = c->plane_w; d.plane_h = c->plane_h;
     d.block = c->block;
     d.pipelines = c->pipelines;
+    d.ray_sort = c->ray_sort;
     return d;
 }
 

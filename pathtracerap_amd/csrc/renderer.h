@@ -24,6 +24,7 @@ struct RenderConfig {            // Config.h + generateRaysKernel constants, at 
     int grid[3] = {25, 25, 25};           // GRID_X/Y/Z
     int tail_drop = 0;                    // replicate ceil(n/32) launch truncation (Renderer.cpp:573)
     int block = 64;                       // bounce-kernel workgroup size = compaction chunk (64/128/256)
+    int ray_sort = -1;                    // -1 auto (grid_fast: key 7), 0 off, 1..8 key layout (k_sort_hist)
     int pipelines = 8;                    // iterations in flight on their own HIP streams (1..kMaxPipes)
     double cam[3] = {0.0, 0.0, 920.0};    // Renderer.cpp:528
     double plane_z = 900.0;               // Renderer.cpp:543
@@ -71,6 +72,11 @@ struct KParams {
     int* defer_slots;                   // k_trace_gf: slots whose hit set overflowed LDS (k_trace_deferred)
     int* defer_count;                   // reset by k_scan
     float* contrib;                     // pipelines > 1: this pipeline's per-iteration contributions (k_merge)
+    int2* order;                        // ray sort: claim position -> (dense slot, source index); null: claim order
+    int* sort_bins;                     // [kSortBins] rays per key, [kSortBins] scatter cursors; zeroed by k_scan
+    unsigned short* sort_key;           // per source index of the previous bounce's pool
+    int sort_mode;                      // key layout (k_sort_hist); 0 = no sort
+    float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
 };

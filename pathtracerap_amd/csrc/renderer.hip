@@ -51,6 +51,8 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
+constexpr int kSortBits = 12, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
+constexpr int kSortWG = 1024, kSortPer = 4;                 // source indices per sort workgroup: 4096
 
 // ---------------------------------------------------------------------------
 // Device helpers
@@ -1137,7 +1139,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 if (state == 0) {
                     j = base + __popcll(idle & ((1ull << lane) - 1ull));
                     if (j < n) {
-                        const int src = slot_source(p, j);
+                        int src;
+                        if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
+                        else src = slot_source(p, j);
                         const float4 a = p.ray[in_buf][0][src];
                         const float4 b = p.ray[in_buf][1][src];
                         ow = mk3(a.x, a.y, a.z);
@@ -1478,7 +1482,9 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (state == 0) {
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
-                    const int src = slot_source(p, j);
+                    int src;
+                    if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
+                    else src = slot_source(p, j);
                     const float4 a = p.ray[in_buf][0][src];
                     const float4 b = p.ray[in_buf][1][src];
                     ow = mk3(a.x, a.y, a.z);
@@ -1923,6 +1929,8 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
         *p.defer_count = 0;        // and no deferred grid_fast rays
     }
+    if (p.order)                   // empty key histogram and cursors for the next bounce's ray sort
+        for (int i = tid; i < 2 * kSortBins; i += 1024) p.sort_bins[i] = 0;
 }
 
 // Slot map for bounce+1: dense slot blk_off[b] + r <- source index b * chunk + r
@@ -1934,6 +1942,144 @@ __global__ __launch_bounds__(256) void k_slotmap(KParams p, int bounce) {
     if (i >= ((n + CH - 1) / CH) * CH) return;
     const int b = i / CH, r = i - b * CH;
     if (r < p.blk_cnt[b]) p.slot_src[p.blk_off[b] + r] = i;
+}
+
+// ---------------------------------------------------------------------------
+// Ray sort before a persistent trace (bounce >= 1).  The trace result of a ray
+// does not depend on which lane traces it or when, so the claim order is free:
+// a counting sort on a 12-bit (direction, origin) key hands each wave rays that
+// walk the same BLAS nodes (coherent SIMD steps, shared L2 lines).  The dense
+// slot j -- the RNG seed and the hit-buffer index -- is carried, not changed.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
+    // octahedral direction map (u, v in [-1, 1]) quantized to 64 x 64, origin cell 16^3
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float u = d.x / s, v = d.y / s;
+    if (d.z < 0.0f) {
+        const float uu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
+        const float vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
+        u = uu; v = vv;
+    }
+    const int iu = min(63, max(0, (int)((u * 0.5f + 0.5f) * 64.0f)));
+    const int iv = min(63, max(0, (int)((v * 0.5f + 0.5f) * 64.0f)));
+    const int ix = min(15, max(0, (int)((o.x - p.sort_lo[0]) * p.sort_sc[0])));
+    const int iy = min(15, max(0, (int)((o.y - p.sort_lo[1]) * p.sort_sc[1])));
+    const int iz = min(15, max(0, (int)((o.z - p.sort_lo[2]) * p.sort_sc[2])));
+    switch (p.sort_mode) {
+        case 1:   // direction major (8 x 8 cells), origin 4^3 minor
+            return ((iu >> 3) << 9) | ((iv >> 3) << 6) | ((ix >> 2) << 4) | ((iy >> 2) << 2) | (iz >> 2);
+        case 2:   // origin 4^3 major, direction 8 x 8 minor
+            return ((ix >> 2) << 10) | ((iy >> 2) << 8) | ((iz >> 2) << 6) | ((iu >> 3) << 3) | (iv >> 3);
+        case 4:   // direction only, 64 x 64
+            return (iu << 6) | iv;
+        case 5:   // origin only, 16^3
+            return (ix << 8) | (iy << 4) | iz;
+        case 6: { // origin 8^3 (interleaved) major, direction octant minor
+            const int x = ix >> 1, y = iy >> 1, z = iz >> 1;
+            int m = 0;
+            for (int q = 2; q >= 0; q--) m = (m << 3) | (((x >> q) & 1) << 2) | (((y >> q) & 1) << 1) | ((z >> q) & 1);
+            return (m << 3) | ((d.x < 0.0f) << 2) | ((d.y < 0.0f) << 1) | (d.z < 0.0f);
+        }
+        case 7: { // interleaved, origin first: x1 y1 z1 u2 v2 x0 y0 z0 u1 v1 u0 v0
+            const int a = iu >> 3, b = iv >> 3, x = ix >> 2, y = iy >> 2, z = iz >> 2;
+            return (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) | (((z >> 1) & 1) << 9) | (((a >> 2) & 1) << 8) |
+                   (((b >> 2) & 1) << 7) | ((x & 1) << 6) | ((y & 1) << 5) | ((z & 1) << 4) | (((a >> 1) & 1) << 3) |
+                   (((b >> 1) & 1) << 2) | ((a & 1) << 1) | (b & 1);
+        }
+        case 8: { // interleaved, direction 16 x 16 and origin 2^3... : u3 v3 x0 y0 z0 u2 v2 u1 v1 u0 v0 + pad
+            const int a = iu >> 2, b = iv >> 2, x = ix >> 3, y = iy >> 3, z = iz >> 3;
+            return (((a >> 3) & 1) << 10) | (((b >> 3) & 1) << 9) | (x << 8) | (y << 7) | (z << 6) |
+                   (((a >> 2) & 1) << 5) | (((b >> 2) & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) |
+                   ((a & 1) << 1) | (b & 1);
+        }
+        default: { // interleaved: u2 v2 x1 y1 z1 u1 v1 x0 y0 z0 u0 v0 (u, v: 3 bits, x, y, z: 2 bits)
+            const int a = iu >> 3, b = iv >> 3, x = ix >> 2, y = iy >> 2, z = iz >> 2;
+            return (((a >> 2) & 1) << 11) | (((b >> 2) & 1) << 10) | (((x >> 1) & 1) << 9) | (((y >> 1) & 1) << 8) |
+                   (((z >> 1) & 1) << 7) | (((a >> 1) & 1) << 6) | (((b >> 1) & 1) << 5) | ((x & 1) << 4) |
+                   ((y & 1) << 3) | ((z & 1) << 2) | ((a & 1) << 1) | (b & 1);
+        }
+    }
+}
+
+// Rays entering bounce `bounce` sit at source index i = c*chunk + r (r < blk_cnt[c]) of
+// the previous bounce's pool; dense slot j = blk_off[c] + r.
+__global__ __launch_bounds__(kSortWG) void k_sort_hist(KParams p, int bounce) {
+    __shared__ int s_h[kSortBins];
+    const int nprev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
+    const int lim = ((nprev + p.chunk - 1) / p.chunk) * p.chunk;
+    const int i0 = blockIdx.x * (kSortWG * kSortPer);
+    if (i0 >= lim) return;                               // uniform
+    for (int b = threadIdx.x; b < kSortBins; b += kSortWG) s_h[b] = 0;
+    __syncthreads();
+    const int in_buf = (bounce + 1) & 1;
+#pragma unroll
+    for (int t = 0; t < kSortPer; t++) {
+        const int i = i0 + t * kSortWG + threadIdx.x;
+        if (i < lim) {
+            const int c = i / p.chunk, r = i - c * p.chunk;
+            if (r < p.blk_cnt[c]) {
+                const float4 a = p.ray[in_buf][0][i];
+                const float4 b = p.ray[in_buf][1][i];
+                const int key = sort_key(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
+                p.sort_key[i] = (unsigned short)key;
+                atomicAdd(&s_h[key], 1);
+            }
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kSortBins; b += kSortWG)
+        if (s_h[b]) atomicAdd(&p.sort_bins[b], s_h[b]);
+}
+
+__global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce) {
+    __shared__ int s_start[kSortBins];                   // global exclusive prefix of the bin counts
+    __shared__ int s_h[kSortBins];                       // local counts, then this workgroup's base per bin
+    __shared__ int s_part[kSortWG];
+    const int nprev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
+    const int lim = ((nprev + p.chunk - 1) / p.chunk) * p.chunk;
+    const int i0 = blockIdx.x * (kSortWG * kSortPer);
+    if (i0 >= lim) return;
+    constexpr int kPerT = kSortBins / kSortWG;           // 4 bins per thread
+    const int tid = threadIdx.x;
+    int v[kPerT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPerT; q++) { v[q] = p.sort_bins[tid * kPerT + q]; sum += v[q]; }
+    s_part[tid] = sum;
+    for (int b = tid; b < kSortBins; b += kSortWG) s_h[b] = 0;
+    __syncthreads();
+    for (int off = 1; off < kSortWG; off <<= 1) {
+        const int x = tid >= off ? s_part[tid - off] : 0;
+        __syncthreads();
+        s_part[tid] += x;
+        __syncthreads();
+    }
+    int acc = s_part[tid] - sum;
+#pragma unroll
+    for (int q = 0; q < kPerT; q++) { s_start[tid * kPerT + q] = acc; acc += v[q]; }
+    int key[kSortPer], rank[kSortPer], jj[kSortPer];
+#pragma unroll
+    for (int t = 0; t < kSortPer; t++) {
+        const int i = i0 + t * kSortWG + tid;
+        key[t] = -1; rank[t] = 0; jj[t] = 0;
+        if (i < lim) {
+            const int c = i / p.chunk, r = i - c * p.chunk;
+            if (r < p.blk_cnt[c]) {
+                key[t] = p.sort_key[i];
+                jj[t] = p.blk_off[c] + r;
+                rank[t] = atomicAdd(&s_h[key[t]], 1);
+            }
+        }
+    }
+    __syncthreads();
+    for (int b = tid; b < kSortBins; b += kSortWG) {
+        const int c = s_h[b];
+        if (c) s_h[b] = s_start[b] + atomicAdd(&p.sort_bins[kSortBins + b], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kSortPer; t++)
+        if (key[t] >= 0) p.order[s_h[key[t]] + rank[t]] = make_int2(jj[t], i0 + t * kSortWG + tid);
 }
 
 __global__ void k_selftest_math(int n, const float* x, const float* y, float* out) {
@@ -2089,7 +2235,21 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.spill_stride = spills ? trace_blocks * 64 : 1;
         const char* sm = std::getenv("PT_SLOTMAP");
         kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
+        // Ray sort before each persistent trace (claim order only; results unchanged).
+        const char* so = std::getenv("PT_SORT");
+        const bool block_claims = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & 4) : (kp.trace_flags & 4);
+        const int want = so ? std::atoi(so) : cfg.ray_sort >= 0 ? cfg.ray_sort : (cfg.accel == ACCEL_GRID_FAST ? 7 : 0);
+        kp.sort_mode = (split_trace && !block_claims) ? std::max(0, std::min(8, want)) : 0;
+        float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
+        for (const ModelRec& m : scene.model_recs)
+            for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], m.wbox[a]); hi[a] = std::max(hi[a], m.wbox[3 + a]); }
+        for (int a = 0; a < 3; a++) {
+            const float ext = hi[a] - lo[a];
+            kp.sort_lo[a] = ext > 0.0f && ext < 1e30f ? lo[a] : 0.0f;
+            kp.sort_sc[a] = ext > 0.0f && ext < 1e30f ? 16.0f / ext : 0.0f;
+        }
     }
+    kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr;
     PT_HIP(upload(allocs, &kp.segments, nullptr, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.segments, 0, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     // Pipelines: iterations in flight on their own streams, each with its own
@@ -2139,6 +2299,12 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(upload(allocs, &k.defer_count, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.defer_count, 0, sizeof(int), st));
     PT_HIP(upload(allocs, &k.slot_src, nullptr, (k.use_slotmap ? cap : 1) * sizeof(int), st));
+    if (k.sort_mode) {
+        PT_HIP(upload(allocs, &k.order, nullptr, cap * sizeof(int2), st));
+        PT_HIP(upload(allocs, &k.sort_key, nullptr, cap * sizeof(unsigned short), st));
+        PT_HIP(upload(allocs, &k.sort_bins, nullptr, 2 * kSortBins * sizeof(int), st));
+        PT_HIP(hipMemsetAsync(k.sort_bins, 0, 2 * kSortBins * sizeof(int), st));
+    }
     const size_t hcap = split_trace ? cap : 1;
     PT_HIP(upload(allocs, &k.hit4, nullptr, hcap * sizeof(float4), st));
     PT_HIP(upload(allocs, &k.hitm, nullptr, hcap * sizeof(int), st));
@@ -2257,6 +2423,11 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             if (b > 0 && split_trace) {
+                if (k.order) {
+                    const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
+                    hipLaunchKernelGGL(k_sort_hist, sg, dim3(kSortWG), 0, st, k, b);
+                    hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
+                }
                 launchTrace(k, st, b);
                 PT_HIP(hipGetLastError());
                 if (profiling) {
