@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--accel", choices=["bvh", "grid", "grid_fast"], default="grid_fast",
                     help="grid_fast: the reference's grid results (bit-identical), BVH-accelerated; "
@@ -55,9 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
-    ap.add_argument("--pipelines", type=int, default=0,
-                    help="iterations in flight on their own HIP streams (0: the library default)")
-    ap.add_argument("--hw-queues", type=int, default=8,
+    ap.add_argument("--pipelines", type=int, default=16,
+                    help="iterations in flight on their own HIP streams (0: the library default, 8)")
+    ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES for this process (HIP default 4): one hardware queue per "
                          "pipeline stream so iterations in flight do not serialise on a shared queue (max 32)")
     return ap.parse_args()
