@@ -166,6 +166,7 @@ struct Builder {
 void Scene::buildBvh(int mesh) {
     const Mesh& m = meshes[mesh];
     const int ts = m.triangle_indices.start_index, te = m.triangle_indices.end_index;
+    const int n0 = (int)bvh_nodes.size();     // this mesh's nodes are [n0, end)
     std::vector<Ref> refs;
     refs.reserve(te - ts);
     const double e = (double)kEps;
@@ -227,7 +228,50 @@ void Scene::buildBvh(int mesh) {
             root = c.link;
         }
     }
-    mesh_bvh_root[mesh] = root;
+    mesh_bvh_root[mesh] = relayoutPairs(n0, root);
+}
+
+// Node order for the traversal's memory system: the two inner children of a
+// node are stored side by side in one 128-byte line (an even node index; a
+// padding node keeps the pairing), pairs in depth-first order.  A visit that
+// fetches one child's record brings its sibling's, usually visited next, into
+// L2 with it.  Only addresses change: boxes, links' targets, traversal order
+// and results do not.  PT_BVH_PAIRS=0 keeps the plain pre-order.
+int Scene::relayoutPairs(int n0, int root) {
+    static const bool on = [] {
+        const char* e = std::getenv("PT_BVH_PAIRS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const int n1 = (int)bvh_nodes.size();
+    if (!on || n1 - n0 <= 1) return root;
+    std::vector<BvhNode> out;
+    out.reserve((size_t)(n1 - n0) * 5 / 4 + 2);
+    std::vector<int> nid(n1 - n0, -1);
+    auto place = [&](int old) { nid[old - n0] = n0 + (int)out.size(); out.push_back(bvh_nodes[old]); };
+    BvhNode pad_node;
+    std::memset(&pad_node, 0, sizeof pad_node);
+    pad_node.count0 = pad_node.count1 = -1;
+    pad_node.link0 = pad_node.link1 = -1;
+    for (int k = 0; k < 3; k++) { pad_node.lo0[k] = pad_node.lo1[k] = 1.0f; pad_node.hi0[k] = pad_node.hi1[k] = -1.0f; }
+    place(root);
+    std::vector<int> st{root};
+    while (!st.empty()) {
+        const BvhNode nd = bvh_nodes[st.back()];
+        st.pop_back();
+        const bool in0 = nd.count0 == 0, in1 = nd.count1 == 0;
+        if (in0 && in1 && ((n0 + (int)out.size()) & 1)) out.push_back(pad_node);
+        if (in0) place(nd.link0);
+        if (in1) place(nd.link1);
+        if (in1) st.push_back(nd.link1);
+        if (in0) st.push_back(nd.link0);
+    }
+    for (BvhNode& nd : out) {
+        if (nd.count0 == 0) nd.link0 = nid[nd.link0 - n0];
+        if (nd.count1 == 0) nd.link1 = nid[nd.link1 - n0];
+    }
+    bvh_nodes.resize(n0);
+    bvh_nodes.insert(bvh_nodes.end(), out.begin(), out.end());
+    return nid[root - n0];
 }
 
 namespace {

@@ -105,6 +105,7 @@ private:
     void buildDeviceTables();
     void buildBvh(int mesh);
     void buildBvh4(int mesh);
+    int relayoutPairs(int n0, int root);       // sibling inner nodes side by side (bvh.cpp)
     void world_box(const Model& m, const Mesh& mesh, int root, float* out) const;
 };
 
