@@ -2342,7 +2342,8 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b); break;
             default: hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b); break;
         }
-        hipLaunchKernelGGL(k_trace_deferred<64>, g, t, 0, st, k, b);
+        // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
+        hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, 1024)), t, 0, st, k, b);
         return;
     }
     switch (k.trace_flags & 31) {

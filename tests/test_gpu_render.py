@@ -391,3 +391,31 @@ def test_ray_sort_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, accel, mode,
     img, seg, oimg, oseg = _render_both(P, O, s, cfg)
     assert seg == oseg
     assert_bitexact(img, oimg, f"PT_SORT={mode}")
+
+
+def test_bench_configuration_bit_identical(gpu, pt_mod, oracle_mod, synth_dir):
+    """The bench's setup -- caller's stream, caller-owned accumulator, 16
+    pipelines, default ray sort, several renderLoop calls, clearImage between
+    them -- gives the oracle's image bit for bit."""
+    import torch
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=6000, seed=21))
+    s.build(bvh=True)
+    cfg = P.RenderConfig(width=160, height=128, iterations=20, max_bounces=8, accel=2, pipelines=16)
+    img = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    r = P.Renderer(cfg)
+    r.set_stream(st.cuda_stream)
+    r.bind_image(img.data_ptr(), keepalive=img)
+    r.allocateOnGPU(s)
+    assert r.pipelines() == 16
+    r.renderLoop(0, 3, sync=False)          # warm-up iterations, then discarded
+    r.clearImage()
+    r.renderLoop(0, 7, sync=False)
+    r.renderLoop(7, 13, sync=False)
+    st.synchronize()
+    got = img.cpu().numpy().reshape(-1, 3)
+    r.free()
+    want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg))
+    assert_bitexact(got, want, "bench configuration")
