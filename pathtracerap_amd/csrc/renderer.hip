@@ -2032,21 +2032,16 @@ __global__ __launch_bounds__(kSortWG) void k_sort_hist(KParams p, int bounce) {
         if (s_h[b]) atomicAdd(&p.sort_bins[b], s_h[b]);
 }
 
-__global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce) {
-    __shared__ int s_start[kSortBins];                   // global exclusive prefix of the bin counts
-    __shared__ int s_h[kSortBins];                       // local counts, then this workgroup's base per bin
+// One workgroup: cursor[b] = exclusive prefix of the key counts (the first claim
+// position of key b); k_sort_scatter's workgroups reserve their ranges from it.
+__global__ __launch_bounds__(kSortWG) void k_sort_prefix(KParams p) {
     __shared__ int s_part[kSortWG];
-    const int nprev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
-    const int lim = ((nprev + p.chunk - 1) / p.chunk) * p.chunk;
-    const int i0 = blockIdx.x * (kSortWG * kSortPer);
-    if (i0 >= lim) return;
     constexpr int kPerT = kSortBins / kSortWG;           // 4 bins per thread
     const int tid = threadIdx.x;
     int v[kPerT], sum = 0;
 #pragma unroll
     for (int q = 0; q < kPerT; q++) { v[q] = p.sort_bins[tid * kPerT + q]; sum += v[q]; }
     s_part[tid] = sum;
-    for (int b = tid; b < kSortBins; b += kSortWG) s_h[b] = 0;
     __syncthreads();
     for (int off = 1; off < kSortWG; off <<= 1) {
         const int x = tid >= off ? s_part[tid - off] : 0;
@@ -2056,7 +2051,18 @@ __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce)
     }
     int acc = s_part[tid] - sum;
 #pragma unroll
-    for (int q = 0; q < kPerT; q++) { s_start[tid * kPerT + q] = acc; acc += v[q]; }
+    for (int q = 0; q < kPerT; q++) { p.sort_bins[kSortBins + tid * kPerT + q] = acc; acc += v[q]; }
+}
+
+__global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce) {
+    __shared__ int s_h[kSortBins];                       // local counts, then this workgroup's base per key
+    const int nprev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
+    const int lim = ((nprev + p.chunk - 1) / p.chunk) * p.chunk;
+    const int i0 = blockIdx.x * (kSortWG * kSortPer);
+    if (i0 >= lim) return;
+    const int tid = threadIdx.x;
+    for (int b = tid; b < kSortBins; b += kSortWG) s_h[b] = 0;
+    __syncthreads();
     int key[kSortPer], rank[kSortPer], jj[kSortPer];
 #pragma unroll
     for (int t = 0; t < kSortPer; t++) {
@@ -2074,7 +2080,7 @@ __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce)
     __syncthreads();
     for (int b = tid; b < kSortBins; b += kSortWG) {
         const int c = s_h[b];
-        if (c) s_h[b] = s_start[b] + atomicAdd(&p.sort_bins[kSortBins + b], c);
+        if (c) s_h[b] = atomicAdd(&p.sort_bins[kSortBins + b], c);   // cursor starts at the key's prefix
     }
     __syncthreads();
 #pragma unroll
@@ -2427,6 +2433,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
                 if (k.order) {
                     const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
                     hipLaunchKernelGGL(k_sort_hist, sg, dim3(kSortWG), 0, st, k, b);
+                    hipLaunchKernelGGL(k_sort_prefix, dim3(1), dim3(kSortWG), 0, st, k);
                     hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
                 }
                 launchTrace(k, st, b);
