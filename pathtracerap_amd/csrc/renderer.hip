@@ -1067,11 +1067,14 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
     int* spill = p.spill + (size_t)blockIdx.x * BS + threadIdx.x;   // stack entries beyond the LDS part
-    const bool lds_models = (F & 1) && p.nmodels <= kLdsModels;
+    // F & 1 is launched only when the scene has at most kLdsModels models: the
+    // choice is compile-time, so model reads are ds_read (LDS) or global loads,
+    // never flat loads through a generic pointer.
+    constexpr bool lds_models = (F & 1) != 0;
     if (lds_models) {
         const int* src = reinterpret_cast<const int*>(p.models);
         int* dst = reinterpret_cast<int*>(s_models);
-        const int nw = p.nmodels * (int)(sizeof(ModelRec) / 4);
+        const int nw = min(p.nmodels, kLdsModels) * (int)(sizeof(ModelRec) / 4);
         for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
         __syncthreads();
     }
@@ -1409,11 +1412,14 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
     int* spill = p.spill + (size_t)blockIdx.x * BS + threadIdx.x;
-    const bool lds_models = (F & 1) && p.nmodels <= kLdsModels;
+    // F & 1 is launched only when the scene has at most kLdsModels models: the
+    // choice is compile-time, so model reads are ds_read (LDS) or global loads,
+    // never flat loads through a generic pointer.
+    constexpr bool lds_models = (F & 1) != 0;
     if (lds_models) {
         const int* src = reinterpret_cast<const int*>(p.models);
         int* dst = reinterpret_cast<int*>(s_models);
-        const int nw = p.nmodels * (int)(sizeof(ModelRec) / 4);
+        const int nw = min(p.nmodels, kLdsModels) * (int)(sizeof(ModelRec) / 4);
         for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
         __syncthreads();
     }
@@ -2223,10 +2229,12 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
         const char* gff = std::getenv("PT_GF_FLAGS");
         gf_flags = gff ? std::atoi(gff) : 9;
+        if (scene.model_recs.size() > (size_t)kLdsModels) gf_flags &= ~1;     // model records stay in global memory
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
         kp.trace_flags = tf ? std::atoi(tf) : 11;
+        if (scene.model_recs.size() > (size_t)kLdsModels) kp.trace_flags &= ~1;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
@@ -2345,8 +2353,12 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b); break;
             case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b); break;
             case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b); break;
+            case 12: hipLaunchKernelGGL((k_trace_gf<64, 12>), g, t, 0, st, k, b); break;
             case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b); break;
-            default: hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b); break;
+            default:                         // 9; 8 when the model records do not fit LDS
+                if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b);
+                else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b);
+                break;
         }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
         hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, 1024)), t, 0, st, k, b);
@@ -2362,9 +2374,14 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
         case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, st, k, b); break;
         case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, st, k, b); break;
         case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b); break;
+        case 26: hipLaunchKernelGGL((k_trace_bvh<64, 26>), g, t, 0, st, k, b); break;
         case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, st, k, b); break;
+        case 18: hipLaunchKernelGGL((k_trace_bvh<64, 18>), g, t, 0, st, k, b); break;
         case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, st, k, b); break;
-        default: hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b); break;
+        default:                             // 11; 10 when the model records do not fit LDS
+            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b);
+            else hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b);
+            break;
     }
 }
 
