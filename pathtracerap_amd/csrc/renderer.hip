@@ -1894,7 +1894,9 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
     const int per = (nb + 1023) / 1024;
     const int s = tid * per, e = min(s + per, nb);
     int sum = 0;
-    for (int i = s; i < e; i++) sum += staged ? s_v[i] : p.blk_cnt[i];
+    // explicit branches (not a pointer select): LDS and global reads, no flat loads
+    if (staged) { for (int i = s; i < e; i++) sum += s_v[i]; }
+    else { for (int i = s; i < e; i++) sum += p.blk_cnt[i]; }
     s_part[tid] = sum;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
@@ -1924,8 +1926,9 @@ __global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
     }
     const int total = s_total;
     for (int i = s; i < e; i++) {
-        const int o0 = staged ? s_v[i] : p.blk_off[i];                  // this thread's own writes
-        const int o1 = staged ? s_v[i + 1] : o0 + p.blk_cnt[i];
+        int o0, o1;
+        if (staged) { o0 = s_v[i]; o1 = s_v[i + 1]; }
+        else { o0 = p.blk_off[i]; o1 = o0 + p.blk_cnt[i]; }             // this thread's own writes
         if (o1 == o0) continue;
         for (int bd = (o0 + CH - 1) / CH; bd * CH < o1; bd++) p.dst_start[bd] = i;
     }
