@@ -32,6 +32,10 @@ def test_abi_version_and_defaults(pt_mod):
     assert (c.width, c.height, c.iterations, c.max_bounces) == (1000, 800, 500, 5)
     assert tuple(c.grid) == (25, 25, 25) and tuple(c.cam) == (0.0, 0.0, 920.0)
     assert (c.plane_x0, c.plane_y0, c.plane_w, c.plane_h, c.plane_z) == (-10.0, -4.0, 20.0, 16.0, 900.0)
+    # throughput knobs (results identical for every value): the struct tail matches the header
+    assert (c.block, c.pipelines, c.ray_sort) == (64, 8, -1)
+    py = pt_mod.RenderConfig()
+    assert (py.block, py.pipelines, py.ray_sort) == (c.block, c.pipelines, c.ray_sort)
 
 
 def test_errors_are_reported_not_crashing(pt_mod):
