@@ -1,10 +1,12 @@
 // renderer.h -- MI355X wavefront renderer (Renderer.h:368-377 mirror).
 //
 // allocateOnGPU / renderLoop / renderImage / free keep the reference's
-// entry points; underneath, each bounce is ONE fused gfx950 kernel
-// (intersect + BSDF scatter + block-local stable compaction + framebuffer
-// accumulate of terminated rays) followed by a one-workgroup block-offset
-// scan -- no host round trip inside an iteration.
+// entry points; underneath, each bounce is a persistent trace kernel
+// (grid_fast / bvh; grid_fast after a counting sort of the live rays) and a
+// shading kernel (BSDF scatter + block-local stable compaction + framebuffer
+// accumulate of terminated rays), then a one-workgroup block-offset scan --
+// no host round trip inside an iteration.  `pipelines` iterations run at once
+// on their own HIP streams; their contributions merge in iteration order.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -5,8 +5,16 @@
 //              compact survivors (block-local, stable) / accumulate the dead
 //   scan     : k_scan           -- one workgroup: exclusive scan of the block
 //              survivor counts -> dense slot numbering for the next bounce
-//   bounce b : k_bounce<rest>   -- gather ray (slot j -> source via the scan),
-//              intersect (grid DDA or BVH), shade, compact / accumulate
+//   bounce b : k_sort_hist / k_sort_prefix / k_sort_scatter (grid_fast) -- claim
+//              order of the live rays by a (origin, direction) key;
+//              k_trace_gf / k_trace_bvh -- persistent trace of every live slot
+//              into the hit buffer (k_trace_deferred: overflowed hit sets);
+//              k_bounce<rest, hitbuf> -- gather ray + hit (slot j -> source via
+//              the scan), shade, compact / accumulate
+//              (PT_GF_SPLIT=0 / PT_TRACE_SPLIT=0: the fused k_bounce<rest, accel>)
+// Iterations run `pipelines` at a time on their own streams (Renderer::renderLoop);
+// with more than one, terminated rays write a per-pipeline contribution buffer
+// that k_merge adds to the image in iteration order.
 // The dense slot j of a ray at bounce b equals its index in the reference's
 // thrust::stable_partition'ed ray pool, so the RNG seed
 // makeSeededRandomEngine(iter, j, remaining_bounces) -- and hence every
