@@ -81,6 +81,7 @@ struct KParams {
     float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
+    int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
 };
 
 constexpr int kMaxBounceCounters = 64;
@@ -124,6 +125,8 @@ private:
     int allocPipe(KParams& k, size_t cap, hipStream_t st);
     int fail(hipError_t e, const char* what);
     void freeBuffers();
+    int enqueueIteration(int q, hipStream_t st, int iter, int passes);
+    void dropGraphs();
 
     KParams kp{};                    // pipeline 0 (and everything the pipelines share)
     hipStream_t stream = nullptr;    // the caller's stream; pipeline 0 runs on it
@@ -133,6 +136,8 @@ private:
     hipStream_t pstream[kMaxPipes]{};    // pstream[0] == stream; 1.. created here
     hipEvent_t merge_ev[kMaxPipes]{};    // last k_merge recorded on each pipeline
     hipEvent_t fork_ev = nullptr;
+    hipGraphExec_t gexec[kMaxPipes]{};   // PT_GRAPH: pipeline i's bounce loop captured once, replayed per iteration
+    bool use_graph = false;
     bool own_stream = false;
     bool stream_set = false;
     bool allocated = false;

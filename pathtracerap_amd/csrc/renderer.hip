@@ -1834,7 +1834,7 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
                 h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
             }
         }
-        shade(p, r, h, iter, j);
+        shade(p, r, h, iter >= 0 ? iter : *p.iter_dev, j);   // -1: hipGraph replay reads the id
     }
     const bool alive = active && r.bounces > 0;
     if (active && !alive) {
@@ -2124,6 +2124,11 @@ __global__ __launch_bounds__(256) void k_merge(float* __restrict__ image, const 
     if (i < n) image[i] += contrib[i];
 }
 
+// hipGraph replay: the iteration id the captured k_bounce launches read
+__global__ void k_set_iter(int* dst, int iter) {
+    if (threadIdx.x == 0) *dst = iter;
+}
+
 __global__ void k_zero(float* a, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) a[i] = 0.0f;
@@ -2164,6 +2169,7 @@ int Renderer::bindImage(float* device_rgb) {
     if (allocated) {
         kp.image = device_rgb;
         for (int i = 0; i < kMaxPipes; i++) pk[i].image = device_rgb;
+        dropGraphs();                 // captured launches hold the old image pointer
     }
     return 0;
 }
@@ -2300,6 +2306,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     if (!fork_ev) PT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     kp = pk[0];
     PT_HIP(hipStreamSynchronize(stream));
+    const char* gr = std::getenv("PT_GRAPH");
+    use_graph = gr && std::atoi(gr) != 0;
     allocated = true;
     cache_valid = false;
     return clearImage();
@@ -2335,6 +2343,7 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(upload(allocs, &k.hitm, nullptr, hcap * sizeof(int), st));
     PT_HIP(upload(allocs, &k.trace_next, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.trace_next, 0, sizeof(int), st));
+    PT_HIP(upload(allocs, &k.iter_dev, nullptr, sizeof(int), st));
     return 0;
 }
 
@@ -2423,6 +2432,57 @@ void Renderer::launchBounce(const KParams& k, hipStream_t st, bool first, dim3 g
     }
 }
 
+// One iteration's bounce loop on pipeline q (stream st): sort / trace / shade /
+// scan per bounce.  iter = -1: k_bounce reads the id from k.iter_dev (capture).
+int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
+    const KParams& k = pk[q];
+    const dim3 grid((unsigned)kp.nblocks + 8u);
+    for (int b = 0; b < passes; b++) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+        if (b > 0 && split_trace) {
+            if (k.order) {
+                const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
+                hipLaunchKernelGGL(k_sort_hist, sg, dim3(kSortWG), 0, st, k, b);
+                hipLaunchKernelGGL(k_sort_prefix, dim3(1), dim3(kSortWG), 0, st, k);
+                hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
+            }
+            launchTrace(k, st, b);
+            PT_HIP(hipGetLastError());
+            if (profiling) {
+                hipEventRecord(e1, st);
+                trace_events.push_back({e0, e1});
+                hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st);
+            }
+            launchBounce(k, st, false, grid, iter, b, kAccelHitBuffer);
+        } else {
+            launchBounce(k, st, b == 0, grid, iter, b, cfg.accel);
+        }
+        PT_HIP(hipGetLastError());
+        if (profiling) {
+            hipEventRecord(e1, st);
+            (b == 0 ? first_events : bounce_events).push_back({e0, e1});
+            e0 = e1 = nullptr;
+        }
+        if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, k, b);
+        PT_HIP(hipGetLastError());
+        if (k.use_slotmap && b + 1 < passes) {
+            hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((k.nblocks * k.chunk + 255) / 256)), dim3(256), 0, st, k, b);
+            PT_HIP(hipGetLastError());
+        }
+        if (profiling) { hipEventRecord(e1, st); scan_events.push_back({e0, e1}); }
+    }
+    return 0;
+}
+
+void Renderer::dropGraphs() {
+    for (int i = 0; i < kMaxPipes; i++) {
+        if (gexec[i]) hipGraphExecDestroy(gexec[i]);
+        gexec[i] = nullptr;
+    }
+}
+
 int Renderer::renderLoop(int first_iter, int n_iters) {
     if (!allocated) { last_error = "renderLoop before allocateOnGPU"; return -1; }
     if (n_iters < 0 || first_iter < 0) { last_error = "bad iteration range"; return -1; }
@@ -2441,7 +2501,6 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             hipEventDestroy(e0); hipEventDestroy(e1);
         }
     }
-    const dim3 grid((unsigned)kp.nblocks + 8u);
     const int passes = cfg.max_bounces > 1 ? cfg.max_bounces : 1;
     const int np = npipes;
     if (np > 1) {                                   // fork the pipeline streams off the caller's stream
@@ -2454,41 +2513,26 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
         const int q = it % np;
         const KParams& k = pk[q];
         hipStream_t st = q == 0 ? stream : pstream[q];
-        for (int b = 0; b < passes; b++) {
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
-            if (b > 0 && split_trace) {
-                if (k.order) {
-                    const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
-                    hipLaunchKernelGGL(k_sort_hist, sg, dim3(kSortWG), 0, st, k, b);
-                    hipLaunchKernelGGL(k_sort_prefix, dim3(1), dim3(kSortWG), 0, st, k);
-                    hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
-                }
-                launchTrace(k, st, b);
-                PT_HIP(hipGetLastError());
-                if (profiling) {
-                    hipEventRecord(e1, st);
-                    trace_events.push_back({e0, e1});
-                    hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st);
-                }
-                launchBounce(k, st, false, grid, iter, b, kAccelHitBuffer);
-            } else {
-                launchBounce(k, st, b == 0, grid, iter, b, cfg.accel);
-            }
+        if (use_graph && !profiling && st) {   // (no capture on the legacy null stream)
+            // The bounce loop's launches are identical every iteration but for the
+            // iteration id: capture them once per pipeline (k_bounce reads the id from
+            // k.iter_dev) and replay the graph after one k_set_iter.
+            hipLaunchKernelGGL(k_set_iter, dim3(1), dim3(64), 0, st, k.iter_dev, iter);
             PT_HIP(hipGetLastError());
-            if (profiling) {
-                hipEventRecord(e1, st);
-                (b == 0 ? first_events : bounce_events).push_back({e0, e1});
-                e0 = e1 = nullptr;
+            if (!gexec[q]) {
+                PT_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+                const int rc = enqueueIteration(q, st, -1, passes);
+                hipGraph_t g = nullptr;
+                const hipError_t ec = hipStreamEndCapture(st, &g);
+                if (rc != 0) { if (g) hipGraphDestroy(g); return -1; }
+                PT_HIP(ec);
+                const hipError_t ei = hipGraphInstantiate(&gexec[q], g, nullptr, nullptr, 0);
+                hipGraphDestroy(g);
+                PT_HIP(ei);
             }
-            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
-            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, k, b);
-            PT_HIP(hipGetLastError());
-            if (k.use_slotmap && b + 1 < passes) {
-                hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((k.nblocks * k.chunk + 255) / 256)), dim3(256), 0, st, k, b);
-                PT_HIP(hipGetLastError());
-            }
-            if (profiling) { hipEventRecord(e1, st); scan_events.push_back({e0, e1}); }
+            PT_HIP(hipGraphLaunch(gexec[q], st));
+        } else if (enqueueIteration(q, st, iter, passes) != 0) {
+            return -1;
         }
         if (np > 1) {
             // image += this iteration's contributions, after the previous iteration's merge
@@ -2679,6 +2723,7 @@ void Renderer::freeBuffers() {
     if (allocated || stream) hipStreamSynchronize(stream);
     for (int i = 1; i < kMaxPipes; i++)
         if (pstream[i]) hipStreamSynchronize(pstream[i]);
+    dropGraphs();
     for (void* p : allocs) hipFree(p);
     allocs.clear();
     kp.image = nullptr;

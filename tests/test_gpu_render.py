@@ -419,3 +419,37 @@ def test_bench_configuration_bit_identical(gpu, pt_mod, oracle_mod, synth_dir):
     r.free()
     want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg))
     assert_bitexact(got, want, "bench configuration")
+
+
+@pytest.mark.parametrize("accel,pipes", [(0, 1), (1, 1), (2, 1), (1, 16), (2, 16), (2, 3)])
+def test_graph_replay_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, pipes):
+    """PT_GRAPH=1: each pipeline's bounce loop is captured once into a hipGraph
+    and replayed per iteration (k_bounce reads the iteration id from device
+    memory).  Image and segment counts stay the oracle's bit for bit across
+    several renderLoop calls, a clearImage, and a caller-owned stream."""
+    import torch
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_GRAPH", "1")
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=3000, seed=9, metallic=True))
+    s.build(bvh=accel != 0)
+    cfg = P.RenderConfig(width=97, height=61, iterations=9, max_bounces=6, accel=accel, pipelines=pipes)
+    img = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    r = P.Renderer(cfg)
+    r.set_stream(st.cuda_stream)
+    r.bind_image(img.data_ptr(), keepalive=img)
+    r.allocateOnGPU(s)
+    r.renderLoop(0, 2, sync=False)          # captures the graphs, then discarded
+    r.clearImage()
+    st.synchronize()
+    seg0 = r.segments()
+    r.renderLoop(0, 4, sync=False)
+    r.renderLoop(4, 5, sync=False)
+    st.synchronize()
+    seg = r.segments() - seg0
+    got = img.cpu().numpy().reshape(-1, 3)
+    r.free()
+    want, oseg = O.render(flat_from_export(s.export(), cfg.grid), oracle_cfg(cfg))
+    assert seg == oseg
+    assert_bitexact(got, want, f"PT_GRAPH accel={accel} pipes={pipes}")
