@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event pass")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-rank path with several ranks on one GPU)")
     ap.add_argument("--pipelines", type=int, default=16,
                     help="iterations in flight on their own HIP streams (0: the library default, 8)")
     ap.add_argument("--hw-queues", type=int, default=16,
@@ -137,10 +140,15 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on a 1-GPU
+    # box) ranks share devices round-robin
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -315,7 +323,7 @@ def main():
                        "spp_per_step": 1, "accel": args.accel,
                        "results": "bit-identical to the reference algorithm (oracle-checked)"
                        if args.accel != "bvh" else "exact closest hit",
-                       "parallelism": f"samples sharded x{world}", "pipelines": pipes,
+                       "parallelism": f"samples sharded x{world}" + (" (gloo rehearsal)" if world > 1 and args.dist_backend == "gloo" else ""), "pipelines": pipes,
                        "segments": int(seg_total), "segments_per_bounce_rank0": per_bounce,
                        "image_finite": img_ok},
             "roofline": roof, "cpu_baseline": cpu, "alt_mode": alt,
