@@ -1563,6 +1563,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 ninv = node_inv(inv);
                 G = mk3((M.vw[0] + M.cslack[0]) * absr(ninv.x), (M.vw[1] + M.cslack[1]) * absr(ninv.y),
                         (M.vw[2] + M.cslack[2]) * absr(ninv.z));
+                if (PT_TRACE_STATS && (p.debug & 512)) G = G * 0.5f;   // timing-only ablation: half-voxel growth
+                if (PT_TRACE_STATS && (p.debug & 1024)) G = mk3(0, 0, 0);   // timing-only ablation: no growth
                 tier = 0;
                 win = (PT_TRACE_STATS && (p.debug & 256)) ? 0.0f : M.wdelta;   // 256: timing-only ablation
                 cur = M.bvh_root;
