@@ -194,6 +194,9 @@ def main():
     t1 = time.perf_counter()
 
     seg = r.segments() - seg0
+    faults = r.trace_faults()
+    if faults:   # a persistent trace gave up: rays kept stale hits, the measured image is wrong
+        raise SystemExit(f"bench: {faults} persistent-trace wave(s) hit the iteration cap; result invalid")
     per_bounce = [a - b for a, b in zip(r.segments_per_bounce(), pb0)]
     while per_bounce and per_bounce[-1] == 0:
         per_bounce.pop()
@@ -254,6 +257,8 @@ def main():
             dist.barrier()
         a1 = time.perf_counter()
         seg2 = float(r2.segments() - s2)
+        if r2.trace_faults():
+            raise SystemExit(f"bench: alt mode {args.alt_accel}: persistent trace hit the iteration cap")
         r2.free()
         ta = torch.tensor([a1 - a0, seg2], dtype=torch.float64, device=dev)
         if world > 1:
@@ -325,7 +330,7 @@ def main():
                        if args.accel != "bvh" else "exact closest hit",
                        "parallelism": f"samples sharded x{world}" + (" (gloo rehearsal)" if world > 1 and args.dist_backend == "gloo" else ""), "pipelines": pipes,
                        "segments": int(seg_total), "segments_per_bounce_rank0": per_bounce,
-                       "image_finite": img_ok},
+                       "image_finite": img_ok, "trace_faults": faults},
             "roofline": roof, "cpu_baseline": cpu, "alt_mode": alt,
         }
         print(json.dumps(out), flush=True)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2
+#define PT_ABI_VERSION 3
 
 /* Primitive.h:213-222 Material::MaterialType */
 enum {
@@ -121,6 +121,10 @@ int pt_renderer_read_image(pt_renderer *r, float *host_rgb);
 int pt_renderer_render_image(pt_renderer *r, const char *bmp_path, int iterations_total);
 /* Ray segments shaded so far (sum over bounces of live rays). */
 long long pt_renderer_segments(pt_renderer *r);
+/* Persistent-trace waves that hit their iteration cap and left rays untraced since
+ * allocate_on_gpu (0 in a correct run; -1 on error).  Non-zero makes
+ * pt_renderer_synchronize / read_image / render_image fail: the image is invalid. */
+long long pt_renderer_trace_faults(pt_renderer *r);
 /* out[b] = live rays entering bounce b, summed over the iterations rendered (b < n, n <= 64 useful). */
 int pt_renderer_segments_per_bounce(pt_renderer *r, long long *out, int n);
 int pt_renderer_set_profiling(pt_renderer *r, int on);

@@ -93,6 +93,7 @@ EXPORTS = [
     ("pt_renderer_read_image", ctypes.c_int, [ctypes.c_void_p, _P_F]),
     ("pt_renderer_render_image", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     ("pt_renderer_segments", ctypes.c_longlong, [ctypes.c_void_p]),
+    ("pt_renderer_trace_faults", ctypes.c_longlong, [ctypes.c_void_p]),
     ("pt_renderer_segments_per_bounce", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("pt_renderer_pipelines", ctypes.c_int, [ctypes.c_void_p]),
     ("pt_renderer_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -321,6 +322,11 @@ class Renderer:
     def segments(self) -> int:
         v = lib().pt_renderer_segments(self._h)
         return _err(v, "segments")
+
+    def trace_faults(self) -> int:
+        """Persistent-trace waves that gave up at the iteration cap (0 in a correct
+        run; non-zero also makes synchronize() / image() raise)."""
+        return _err(lib().pt_renderer_trace_faults(self._h), "trace_faults")
 
     def segments_per_bounce(self, n: int = 64) -> list:
         out = (ctypes.c_longlong * n)()

@@ -217,6 +217,12 @@ long long pt_renderer_segments(pt_renderer* r) {
     if (!r || !r->r) { set_err("null renderer"); return -1; }
     return r->r->segments();
 }
+long long pt_renderer_trace_faults(pt_renderer* r) {
+    if (!r || !r->r) { set_err("null renderer"); return -1; }
+    const long long f = r->r->traceFaults();
+    if (f < 0) set_err("reading the trace fault counter failed");
+    return f;
+}
 int pt_renderer_segments_per_bounce(pt_renderer* r, long long* out, int n) {
     if (!out || n < 0) return set_err("bad arguments");
     R_CALL(r->r->segmentsPerBounce(out, n));

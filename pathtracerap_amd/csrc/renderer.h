@@ -82,10 +82,15 @@ struct KParams {
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
+    unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,
+                                        // counted in segments[kTraceFaultCounter]); PT_TRACE_ITER_CAP overrides
 };
 
 constexpr int kMaxBounceCounters = 64;
 constexpr int kDiagCounters = 64;        // diagnostic counters after the per-bounce ones (PT_TRACE_STATS builds)
+// segments[] slot counting persistent-trace waves that hit trace_iter_cap and left
+// rays untraced (their hit records are stale): any non-zero value invalidates the image
+constexpr int kTraceFaultCounter = 7 + kMaxBounceCounters;
 
 struct KernelStats {
     double bounce_ms = 0, scan_ms = 0, primary_ms = 0, first_ms = 0, trace_ms = 0;
@@ -110,6 +115,7 @@ public:
     int setProfiling(bool on);
     int kernelStats(KernelStats* out);
     long long segments();
+    long long traceFaults();                         // waves that gave up (see kTraceFaultCounter); -1 on error
     int pipelines() const { return npipes; }
     int segmentsPerBounce(long long* out, int n);
     int primaryHits(float* dist, float* normal, int* model);
@@ -127,6 +133,8 @@ private:
     void freeBuffers();
     int enqueueIteration(int q, hipStream_t st, int iter, int passes);
     void dropGraphs();
+    int joinPipes(int np);
+    int checkFaults();
 
     KParams kp{};                    // pipeline 0 (and everything the pipelines share)
     hipStream_t stream = nullptr;    // the caller's stream; pipeline 0 runs on it

@@ -1169,8 +1169,8 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
         }
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
-        if (iters > (1u << 26)) {                       // safety net: never spin forever
-            if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
+        if (iters > p.trace_iter_cap) {                 // safety net: never spin forever (reported as a fault)
+            if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
             break;
         }
         // Phase scheduling (F & 8): one step kind per iteration -- the one most
@@ -1514,8 +1514,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         }
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
-        if (iters > (1u << 26)) {                       // safety net: never spin forever
-            if (lane == 0) atomicAdd(p.segments + 7 + kMaxBounceCounters, 1ull);
+        if (iters > p.trace_iter_cap) {                 // safety net: never spin forever (reported as a fault)
+            if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
             break;
         }
         int phase = 15;
@@ -2169,9 +2169,13 @@ int Renderer::bindImage(float* device_rgb) {
     ext_image = device_rgb;
     external_image = device_rgb != nullptr;
     if (allocated) {
+        // captured launches hold the old image pointer: let every launch already
+        // enqueued (graphs included) finish before their executables are destroyed
+        PT_HIP(hipStreamSynchronize(stream));
+        for (int i = 1; i < npipes; i++) PT_HIP(hipStreamSynchronize(pstream[i]));
+        dropGraphs();
         kp.image = device_rgb;
         for (int i = 0; i < kMaxPipes; i++) pk[i].image = device_rgb;
-        dropGraphs();                 // captured launches hold the old image pointer
     }
     return 0;
 }
@@ -2225,6 +2229,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     {
         const char* dbg = std::getenv("PT_DEBUG_ABLATE");   // timing-only ablations; results become wrong
         kp.debug = dbg ? std::atoi(dbg) : 0;
+        // persistent-trace safety net; tests lower it to exercise the fault report
+        const char* cap = std::getenv("PT_TRACE_ITER_CAP");
+        kp.trace_iter_cap = cap ? (unsigned)std::strtoul(cap, nullptr, 10) : (1u << 26);
     }
     kp.chunk = (cfg.block == 64 || cfg.block == 128 || cfg.block == 256) ? cfg.block : 256;
     kp.nblocks = (npix_all + kp.chunk - 1) / kp.chunk;
@@ -2343,6 +2350,10 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     const size_t hcap = split_trace ? cap : 1;
     PT_HIP(upload(allocs, &k.hit4, nullptr, hcap * sizeof(float4), st));
     PT_HIP(upload(allocs, &k.hitm, nullptr, hcap * sizeof(int), st));
+    // NaN distances / model -1: a record no trace ever wrote (only after a trace
+    // fault, which is reported) shades as a miss instead of indexing the models
+    PT_HIP(hipMemsetAsync(k.hit4, 0xFF, hcap * sizeof(float4), st));
+    PT_HIP(hipMemsetAsync(k.hitm, 0xFF, hcap * sizeof(int), st));
     PT_HIP(upload(allocs, &k.trace_next, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.trace_next, 0, sizeof(int), st));
     PT_HIP(upload(allocs, &k.iter_dev, nullptr, sizeof(int), st));
@@ -2510,7 +2521,10 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
         for (int q = 1; q < np; q++) PT_HIP(hipStreamWaitEvent(pstream[q], fork_ev, 0));
     }
     const size_t n3 = (size_t)cfg.width * cfg.height * 3;
-    for (int it = 0; it < n_iters; it++) {
+    // Every exit after the fork goes through joinPipes, so a later clearImage /
+    // readImage on the caller's stream is ordered after everything enqueued here,
+    // also when an iteration fails to enqueue part way through.
+    auto body = [&](int it) -> int {
         const int iter = first_iter + it;
         const int q = it % np;
         const KParams& k = pk[q];
@@ -2543,17 +2557,27 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
             PT_HIP(hipGetLastError());
             PT_HIP(hipEventRecord(merge_ev[q], st));
         }
+        return 0;
+    };
+    int done = 0;
+    int rc = 0;
+    for (; done < n_iters; done++) {
+        if ((rc = body(done)) != 0) break;
     }
-    if (np > 1 && n_iters > 0) {                    // join: the last merge follows every earlier one
-        PT_HIP(hipStreamWaitEvent(stream, merge_ev[(n_iters - 1) % np], 0));
-        for (int q2 = 1; q2 < np; q2++) {           // and every pipeline's work has been merged
-            PT_HIP(hipStreamWaitEvent(stream, merge_ev[q2], 0));
-        }
-    } else if (np > 1) {
-        for (int q2 = 1; q2 < np; q2++) {           // nothing launched: still join the forked streams
-            PT_HIP(hipEventRecord(merge_ev[q2], pstream[q2]));
-            PT_HIP(hipStreamWaitEvent(stream, merge_ev[q2], 0));
-        }
+    const std::string err = last_error;
+    const int jrc = joinPipes(np);
+    if (rc != 0) { last_error = err; return -1; }     // the first failure is the one reported
+    return jrc;
+}
+
+// Join the forked pipeline streams back into the caller's stream: the caller's
+// stream waits for the last merge (which follows every earlier one) and for
+// everything else enqueued on each pipeline stream since the fork.
+int Renderer::joinPipes(int np) {
+    if (np <= 1) return 0;
+    for (int q2 = 1; q2 < np; q2++) {
+        PT_HIP(hipEventRecord(merge_ev[q2], pstream[q2]));
+        PT_HIP(hipStreamWaitEvent(stream, merge_ev[q2], 0));
     }
     return 0;
 }
@@ -2561,6 +2585,28 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
 int Renderer::synchronize() {
     if (!allocated && !stream) return 0;
     PT_HIP(hipStreamSynchronize(stream));
+    return allocated ? checkFaults() : 0;
+}
+
+long long Renderer::traceFaults() {
+    if (!allocated) return 0;
+    unsigned long long v = 0;
+    if (hipMemcpyAsync(&v, kp.segments + kTraceFaultCounter, sizeof v, hipMemcpyDeviceToHost, stream) != hipSuccess)
+        return -1;
+    if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+    return (long long)v;
+}
+
+// A persistent trace that hit its iteration cap left rays with stale hit
+// records, so the accumulated image is wrong: report it as an error.
+int Renderer::checkFaults() {
+    const long long f = traceFaults();
+    if (f < 0) { last_error = "reading the trace fault counter failed"; return -1; }
+    if (f > 0) {
+        last_error = "persistent trace gave up on " + std::to_string(f) +
+                     " wave(s) (iteration cap): image invalid";
+        return -1;
+    }
     return 0;
 }
 
@@ -2630,7 +2676,7 @@ int Renderer::readImage(float* host_rgb) {
     if (!allocated) { last_error = "not allocated"; return -1; }
     PT_HIP(hipMemcpyAsync(host_rgb, kp.image, (size_t)cfg.width * cfg.height * 3 * sizeof(float), hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
-    return 0;
+    return checkFaults();
 }
 
 // Renderer::renderImage (Renderer.cpp:15-63): 54-byte BMP header, rows written
