@@ -82,6 +82,12 @@ struct KParams {
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
+    int* cont;                          // drain continuations: rays a persistent trace handed on (SoA, stride cont_cap)
+    int cont_cap;
+    int* cont_count;                    // continuation records written (reset by k_scan)
+    int* cont_next;                     // continuation records claimed by the tail launch (reset by k_scan)
+    int drain_dump;                     // hand a wave's rays on once the pool is exhausted and <= this many
+                                        // lanes still trace (0: off; PT_DRAIN_DUMP overrides)
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,
                                         // counted in segments[kTraceFaultCounter]); PT_TRACE_ITER_CAP overrides
 };

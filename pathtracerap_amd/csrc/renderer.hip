@@ -42,6 +42,9 @@ constexpr int kBlock = 256;
 #ifndef PT_WALK_CERT
 #define PT_WALK_CERT 1        // decide the common grid_fast walk from the ray's geometry (walk_certify)
 #endif
+#ifndef PT_CERT_FILTER
+#define PT_CERT_FILTER 1      // walk certificate: U over the members not provably entered after B* (walk_certify)
+#endif
 #ifndef PT_WALK_SKIP
 #define PT_WALK_SKIP 1        // fast-forward the grid_fast walk to the members' union box (walk_skip)
 #endif
@@ -60,7 +63,20 @@ constexpr int kBlock = 256;
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
 constexpr int kSortBits = 12, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
-constexpr int kSortWG = 1024, kSortPer = 4;                 // source indices per sort workgroup: 4096
+#ifndef PT_SORT_WG
+#define PT_SORT_WG 256
+#endif
+#ifndef PT_SCAN_WG
+#define PT_SCAN_WG 256
+#endif
+#ifndef PT_DEFER_WGS
+#define PT_DEFER_WGS 64
+#endif
+// Sort / scan workgroups stay small: at 16 pipelines the persistent traces hold
+// nearly every wave slot, and a workgroup only starts once a CU has room for all
+// of its waves and LDS at once (1024-lane ones starved for hundreds of us).
+constexpr int kSortWG = PT_SORT_WG, kSortPer = 4096 / PT_SORT_WG;   // source indices per sort workgroup: 4096
+constexpr int kScanWG = PT_SCAN_WG, kScanPer = 8;                   // k_scan: one workgroup, tiles of 2048 counts
 
 // ---------------------------------------------------------------------------
 // Device helpers
@@ -615,6 +631,79 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
                                              GetM get, int nh, float tmin, float win, int& tri) {
     int cnt = 0;
     int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
+#define PT_CERT_FAIL(r) { if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 32 + (r) + kMaxBounceCounters, 1ull); return false; }
+#if PT_CERT_FILTER
+    // U is the union over the members the walk might enter no later than B*
+    // (the minimum-t members' union box); members whose box it provably enters
+    // only after B* cannot make a voxel before B*'s first one a hit voxel, so
+    // they stay out of U (see below).  First pass: B*.
+    int blx = 1023, bly = 1023, blz = 1023, bhx = 0, bhy = 0, bhz = 0;
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 e = get(h);
+        if (__int_as_float(e.x) != tmin) continue;
+        cnt++;
+        blx = min(blx, e.z & 1023); bly = min(bly, (e.z >> 10) & 1023); blz = min(blz, (e.z >> 20) & 1023);
+        bhx = max(bhx, e.w & 1023); bhy = max(bhy, (e.w >> 10) & 1023); bhz = max(bhz, (e.w >> 20) & 1023);
+    }
+    if (cnt == 0) PT_CERT_FAIL(0)
+    if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) PT_CERT_FAIL(1)
+    {
+        // sB: exact-ray entry parameter (from pt) of B*.  The walk enters its first
+        // voxel of B* at a computed parameter <= sB + errm (errm: the largest
+        // crossing-parameter error of any axis up to there), so every walk voxel
+        // before it is entered at a parameter <= sB + errm.  A walk voxel W of
+        // member h's box, entered at parameter s, puts the exact ray at s within
+        // cslack + |d| errm of W, i.e. inside h's box grown by that: the grown
+        // box's exact entry g_h <= s.  So g_h > sB + errm (+ rounding slack)
+        // proves h's box holds no walk voxel before B*'s first one.
+        const float pp[3] = {pt.x, pt.y, pt.z}, dv[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z};
+        const int bl[3] = {blx, bly, blz}, bh[3] = {bhx, bhy, bhz};
+        float sB = -3.0e38f, sBo = 3.0e38f;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const float lo = M.bbox[a] + (float)bl[a] * M.vw[a], hi = M.bbox[a] + (float)(bh[a] + 1) * M.vw[a];
+            const float s0 = (lo - pp[a]) * iv[a], s1 = (hi - pp[a]) * iv[a];
+            sB = fmaxf(sB, fminf(s0, s1));
+            sBo = fminf(sBo, fmaxf(s0, s1));
+        }
+        float errm = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const float span = M.vw[a] * (float)p.gdim[a];
+            errm = fmaxf(errm, 4.8e-7f * (float)(p.gdim[a] + 4) * (absr(sB) + 1.0f) +
+                                   1e-6f * (absr(M.bbox[a]) + span + absr(pp[a])) * absr(iv[a]));
+        }
+        // a ray that misses B* exactly, or bounds out of range: every member stays in U
+        const bool use = sB <= sBo && absr(sB) < 1e30f && errm < 1e30f;
+        const float lim = sB + 2.0f * errm + 1e-5f * (absr(sB) + 1.0f);
+#pragma unroll
+        for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+            if (CAP > 0 && h >= nh) break;
+            const int4 e = get(h);
+            bool in = true;
+            if (use && __int_as_float(e.x) != tmin) {
+                float g = -3.0e38f, go = 3.0e38f;
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    const float dl = M.cslack[a] + absr(dv[a]) * errm;
+                    const float lo = M.bbox[a] + (float)((e.z >> (10 * a)) & 1023) * M.vw[a] - dl;
+                    const float hi = M.bbox[a] + (float)(((e.w >> (10 * a)) & 1023) + 1) * M.vw[a] + dl;
+                    const float s0 = (lo - pp[a]) * iv[a], s1 = (hi - pp[a]) * iv[a];
+                    g = fmaxf(g, fminf(s0, s1));
+                    go = fminf(go, fmaxf(s0, s1));
+                }
+                // entered only after B* (a grown box the ray misses is never entered)
+                if ((g > go + 1e-5f * (absr(go) + 1.0f) || g - 1e-5f * (absr(g) + 1.0f) > lim) && absr(g) < 1e30f)
+                    in = false;
+            }
+            if (!in) continue;
+            ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
+            uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
+        }
+    }
+#else
 #pragma unroll
     for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
         if (CAP > 0 && h >= nh) break;
@@ -623,9 +712,9 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
         ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
         uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
     }
-#define PT_CERT_FAIL(r) { if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 32 + (r) + kMaxBounceCounters, 1ull); return false; }
     if (cnt == 0) PT_CERT_FAIL(0)
     if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) PT_CERT_FAIL(1)
+#endif
     const float dd[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z}, pp[3] = {pt.x, pt.y, pt.z};
     const int ul[3] = {ulx, uly, ulz}, uh[3] = {uhx, uhy, uhz};
     float sin = -3.0e38f, sout = 3.0e38f;
@@ -1067,14 +1156,36 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
 constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
 
+// Drain continuations.  Once a persistent trace's pool is exhausted its waves
+// empty out: every lane whose ray is done idles until the wave's longest ray
+// finishes, and at 16 pipelines those half-empty waves hold the wave slots the
+// other pipelines' kernels wait for (35 % of trace wave-iterations ran after
+// exhaustion with 8.5 of 64 lanes busy).  So a wave that has at most
+// drain_dump busy lanes left writes each busy lane's exact traversal state to
+// a continuation record and exits; a second, "tail" launch of the same kernel
+// resumes the records packed 64 to a wave.  Only which lane runs a ray and
+// when changes, so every result is unchanged.  Records are SoA: field f of
+// record r at cont[f * cont_cap + r] (coalesced per wave).  Model-space values
+// (o, d, 1/d, node slopes) are recomputed on resume with the same operations.
+enum {
+    kCJ = 0, kCState, kCIm, kCGdist, kCGmodel, kCGtri, kCOw, kCDw = kCOw + 3, kCCur = kCDw + 3, kCSp, kCLfI, kCLfE,
+    kCLf2I, kCLf2E, kCLfNext, kCSpill, kCX      // kernel-specific fields from kCX on
+};
+constexpr int kContFields = 57;
+
 // F (compile-time variant): 1 = model records in LDS, 2 = leaf triangles as
 // their own steps, 4 = claim source blocks (else: claim slots + search).
-template <int BS, int F>
+// TAIL: the tail launch, which resumes drain continuations instead of claiming rays.
+template <int BS, int F, bool TAIL = false>
 __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, int bounce) {
+    static_assert(kCX + 3 + kStack <= kContFields, "continuation record too small");
     __shared__ int s_stack[kStack * BS];
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
-    int* spill = p.spill + (size_t)blockIdx.x * BS + threadIdx.x;   // stack entries beyond the LDS part
+    int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
+    int* spill = p.spill + sbase;                        // stack entries beyond the LDS part
+    const int ncont = TAIL ? *p.cont_count : 0;
+    if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
     // F & 1 is launched only when the scene has at most kLdsModels models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
     // never flat loads through a generic pointer.
@@ -1107,13 +1218,53 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     float best = kFMax;
     bool any = false, exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
+    unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
     int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // wave's claimed source block (uniform)
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
         if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
-            if (F & 4) {
+            if (TAIL) {                                     // resume continuation records
+                const int cnt = __popcll(idle);
+                const int leader = __ffsll((long long)idle) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(p.cont_next, cnt);
+                base = __shfl(base, leader);
+                if (base + cnt >= ncont) exhausted = true;
+                if (state == 0) {
+                    const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
+                    if (r < ncont) {
+                        const int* C = p.cont + r;
+                        const size_t cs = (size_t)p.cont_cap;
+                        j = C[kCJ * cs]; state = C[kCState * cs]; im = C[kCIm * cs];
+                        gdist = __int_as_float(C[kCGdist * cs]); gmodel = C[kCGmodel * cs]; gtri = C[kCGtri * cs];
+                        ow = mk3(__int_as_float(C[kCOw * cs]), __int_as_float(C[(kCOw + 1) * cs]),
+                                 __int_as_float(C[(kCOw + 2) * cs]));
+                        dw = mk3(__int_as_float(C[kCDw * cs]), __int_as_float(C[(kCDw + 1) * cs]),
+                                 __int_as_float(C[(kCDw + 2) * cs]));
+                        cur = C[kCCur * cs]; sp = C[kCSp * cs];
+                        lf_i = C[kCLfI * cs]; lf_e = C[kCLfE * cs]; lf2_i = C[kCLf2I * cs]; lf2_e = C[kCLf2E * cs];
+                        lf_next = C[kCLfNext * cs];
+                        sbase = C[kCSpill * cs];
+                        spill = p.spill + sbase;
+                        best = __int_as_float(C[kCX * cs]); best_tri = C[(kCX + 1) * cs]; any = C[(kCX + 2) * cs] != 0;
+#pragma unroll 1
+                        for (int q = 0; q < kStack; q++) stack[q * BS] = C[(kCX + 3 + q) * cs];
+                        winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                        dlen = sqrtf(dot(dw, dw));
+                        if (state != 1) {                   // inside model im: its model-space ray, as selected
+                            const ModelRec& M = models[im];
+                            o = xform12(M.w2m, ow, 1.0f);
+                            d = normalize(xform12(M.w2m, dw, 0.0f));
+                            const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+                            ninv = node_inv(inv);
+                        }
+                    } else {
+                        state = 3;
+                    }
+                }
+            } else if (F & 4) {
                 for (int guard = 0; guard < 4 && idle; guard++) {
                     if (q_pos >= q_cnt) {                           // claim the next non-empty source block
                         int b = 0;
@@ -1181,11 +1332,44 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                       c4 = __popcll(__ballot(state == 4));
             phase = (c2 >= c4 && c2 >= c1) ? 2 : (c4 >= c1 ? 4 : 1);
         }
+        // drain: at most drain_dump lanes still trace once the pool is exhausted
+        if (!TAIL && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
+            {
+                const unsigned long long nb_ = __popcll(__ballot(state != 0 && state != 3));
+                st_busy += nb_;
+                if (exhausted) { st_drain++; st_drain_busy += nb_; }
+            }
             if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
             if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
             if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
+        }
+        if (phase & 16) {
+            // drain continuation: every busy lane's exact state, then the wave is done
+            const unsigned long long bm = __ballot(state != 3);
+            const int nbusy = __popcll(bm);
+            const int leader = __ffsll((long long)bm) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.cont_count, nbusy);
+            base = __shfl(base, leader);
+            if (state != 3) {
+                int* C = p.cont + base + __popcll(bm & ((1ull << lane) - 1ull));
+                const size_t cs = (size_t)p.cont_cap;
+                C[kCJ * cs] = j; C[kCState * cs] = state; C[kCIm * cs] = im;
+                C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
+                C[kCOw * cs] = __float_as_int(ow.x); C[(kCOw + 1) * cs] = __float_as_int(ow.y);
+                C[(kCOw + 2) * cs] = __float_as_int(ow.z);
+                C[kCDw * cs] = __float_as_int(dw.x); C[(kCDw + 1) * cs] = __float_as_int(dw.y);
+                C[(kCDw + 2) * cs] = __float_as_int(dw.z);
+                C[kCCur * cs] = cur; C[kCSp * cs] = sp;
+                C[kCLfI * cs] = lf_i; C[kCLfE * cs] = lf_e; C[kCLf2I * cs] = lf2_i; C[kCLf2E * cs] = lf2_e;
+                C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = sbase;
+                C[kCX * cs] = __float_as_int(best); C[(kCX + 1) * cs] = best_tri; C[(kCX + 2) * cs] = any ? 1 : 0;
+#pragma unroll 1
+                for (int q = 0; q < kStack; q++) C[(kCX + 3 + q) * cs] = stack[q * BS];
+            }
+            state = 3;
         }
         if ((phase & 1) && state == 1) {                // advance to the next model that survives culling
             for (;;) {
@@ -1339,6 +1523,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     }
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        atomicAdd(p.segments + 44 + kMaxBounceCounters, st_drain);
+        atomicAdd(p.segments + 45 + kMaxBounceCounters, st_drain_busy);
+        atomicAdd(p.segments + 46 + kMaxBounceCounters, st_busy);
         atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
         atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
         atomicAdd(p.segments + 12 + kMaxBounceCounters, st_sel);
@@ -1412,14 +1599,18 @@ __device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3
     tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
 }
 
-template <int BS, int F>
+template <int BS, int F, bool TAIL = false>
 __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce) {
+    static_assert(kCX + 9 + kGfStack + 4 * kGfHitCap <= kContFields, "continuation record too small");
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
-    int* spill = p.spill + (size_t)blockIdx.x * BS + threadIdx.x;
+    int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
+    int* spill = p.spill + sbase;
+    const int ncont = TAIL ? *p.cont_count : 0;
+    if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
     // F & 1 is launched only when the scene has at most kLdsModels models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
     // never flat loads through a generic pointer.
@@ -1450,6 +1641,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
     bool exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
+    unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_walk = 0, it_sel = 0;
     unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
@@ -1457,7 +1649,55 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if ((F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        if (TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+            // resume continuation records
+            const int cnt = __popcll(idle);
+            const int leader = __ffsll((long long)idle) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.cont_next, cnt);
+            base = __shfl(base, leader);
+            if (base + cnt >= ncont) exhausted = true;
+            if (state == 0) {
+                const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
+                if (r < ncont) {
+                    const int* C = p.cont + r;
+                    const size_t cs = (size_t)p.cont_cap;
+                    j = C[kCJ * cs]; state = C[kCState * cs]; im = C[kCIm * cs];
+                    gdist = __int_as_float(C[kCGdist * cs]); gmodel = C[kCGmodel * cs]; gtri = C[kCGtri * cs];
+                    ow = mk3(__int_as_float(C[kCOw * cs]), __int_as_float(C[(kCOw + 1) * cs]),
+                             __int_as_float(C[(kCOw + 2) * cs]));
+                    dw = mk3(__int_as_float(C[kCDw * cs]), __int_as_float(C[(kCDw + 1) * cs]),
+                             __int_as_float(C[(kCDw + 2) * cs]));
+                    cur = C[kCCur * cs]; sp = C[kCSp * cs];
+                    lf_i = C[kCLfI * cs]; lf_e = C[kCLfE * cs]; lf2_i = C[kCLf2I * cs]; lf2_e = C[kCLf2E * cs];
+                    lf_next = C[kCLfNext * cs];
+                    sbase = C[kCSpill * cs];
+                    spill = p.spill + sbase;
+                    tmin = __int_as_float(C[kCX * cs]); nh = C[(kCX + 1) * cs]; tier = C[(kCX + 2) * cs];
+                    pblk = C[(kCX + 3) * cs]; win = __int_as_float(C[(kCX + 4) * cs]);
+                    t_box = __int_as_float(C[(kCX + 5) * cs]);
+                    G = mk3(__int_as_float(C[(kCX + 6) * cs]), __int_as_float(C[(kCX + 7) * cs]),
+                            __int_as_float(C[(kCX + 8) * cs]));
+#pragma unroll 1
+                    for (int q = 0; q < kGfStack; q++) stack[q * BS] = C[(kCX + 9 + q) * cs];
+#pragma unroll 1
+                    for (int q = 0; q < kGfHitCap; q++)
+                        hs[q * BS] = make_int4(C[(kCX + 9 + kGfStack + 4 * q) * cs], C[(kCX + 10 + kGfStack + 4 * q) * cs],
+                                               C[(kCX + 11 + kGfStack + 4 * q) * cs], C[(kCX + 12 + kGfStack + 4 * q) * cs]);
+                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                    dlen = sqrtf(dot(dw, dw));
+                    if (state != 1) {                       // inside model im: its model-space ray, as selected
+                        const ModelRec& M = models[im];
+                        o = xform12(M.w2m, ow, 1.0f);
+                        d = normalize(xform12(M.w2m, dw, 0.0f));
+                        const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+                        ninv = node_inv(inv);
+                    }
+                } else {
+                    state = 3;
+                }
+            }
+        } else if (!TAIL && (F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             // claim whole source blocks of the previous bounce: block b's survivors sit at
             // [b*CH, b*CH + cnt_b) and own dense slots [blk_off[b], blk_off[b] + cnt_b)
             for (int guard = 0; guard < 4 && idle; guard++) {
@@ -1486,7 +1726,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 q_pos += take;
                 idle = __ballot(state == 0);
             }
-        } else if (!(F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        } else if (!TAIL && !(F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
@@ -1527,14 +1767,57 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (c5 > cm) { phase = 8; cm = c5; }
             if (c1 > cm) { phase = 1; cm = c1; }
         }
+        // drain: at most drain_dump lanes still trace once the pool is exhausted
+        if (!TAIL && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
+            {
+                const unsigned long long nb_ = __popcll(__ballot(state != 0 && state != 3));
+                st_busy += nb_;
+                if (exhausted) { st_drain++; st_drain_busy += nb_; }
+            }
             if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
             if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
             if (phase & 8) { st_walk += __popcll(__ballot(state == 5)); it_walk++; }
             if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[0] += t - ts; ts = t; }
+        if (phase & 16) {
+            // drain continuation: every busy lane's exact state, then the wave is done
+            const unsigned long long bm = __ballot(state != 3);
+            const int nbusy = __popcll(bm);
+            const int leader = __ffsll((long long)bm) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.cont_count, nbusy);
+            base = __shfl(base, leader);
+            if (state != 3) {
+                int* C = p.cont + base + __popcll(bm & ((1ull << lane) - 1ull));
+                const size_t cs = (size_t)p.cont_cap;
+                C[kCJ * cs] = j; C[kCState * cs] = state; C[kCIm * cs] = im;
+                C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
+                C[kCOw * cs] = __float_as_int(ow.x); C[(kCOw + 1) * cs] = __float_as_int(ow.y);
+                C[(kCOw + 2) * cs] = __float_as_int(ow.z);
+                C[kCDw * cs] = __float_as_int(dw.x); C[(kCDw + 1) * cs] = __float_as_int(dw.y);
+                C[(kCDw + 2) * cs] = __float_as_int(dw.z);
+                C[kCCur * cs] = cur; C[kCSp * cs] = sp;
+                C[kCLfI * cs] = lf_i; C[kCLfE * cs] = lf_e; C[kCLf2I * cs] = lf2_i; C[kCLf2E * cs] = lf2_e;
+                C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = sbase;
+                C[kCX * cs] = __float_as_int(tmin); C[(kCX + 1) * cs] = nh; C[(kCX + 2) * cs] = tier;
+                C[(kCX + 3) * cs] = pblk; C[(kCX + 4) * cs] = __float_as_int(win);
+                C[(kCX + 5) * cs] = __float_as_int(t_box);
+                C[(kCX + 6) * cs] = __float_as_int(G.x); C[(kCX + 7) * cs] = __float_as_int(G.y);
+                C[(kCX + 8) * cs] = __float_as_int(G.z);
+#pragma unroll 1
+                for (int q = 0; q < kGfStack; q++) C[(kCX + 9 + q) * cs] = stack[q * BS];
+#pragma unroll 1
+                for (int q = 0; q < kGfHitCap; q++) {
+                    const int4 e = hs[q * BS];
+                    C[(kCX + 9 + kGfStack + 4 * q) * cs] = e.x; C[(kCX + 10 + kGfStack + 4 * q) * cs] = e.y;
+                    C[(kCX + 11 + kGfStack + 4 * q) * cs] = e.z; C[(kCX + 12 + kGfStack + 4 * q) * cs] = e.w;
+                }
+            }
+            state = 3;
+        }
         if ((phase & 1) && state == 1) {                // next model that survives culling and the grid entry test
             for (;;) {
                 im++;
@@ -1738,6 +2021,9 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         for (int q = 0; q < 5; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        atomicAdd(p.segments + 44 + kMaxBounceCounters, st_drain);
+        atomicAdd(p.segments + 45 + kMaxBounceCounters, st_drain_busy);
+        atomicAdd(p.segments + 46 + kMaxBounceCounters, st_busy);
         atomicAdd(p.segments + 9 + kMaxBounceCounters, st_node);
         atomicAdd(p.segments + 10 + kMaxBounceCounters, st_leaf);
         atomicAdd(p.segments + 11 + kMaxBounceCounters, st_walk);
@@ -1885,71 +2171,66 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
 
 // One workgroup: exclusive scan of survivor counts of bounce `bounce`,
 // live count for bounce+1, and the first source block of every
-// destination block (dst_start).
-__global__ __launch_bounds__(1024) void k_scan(KParams p, int bounce) {
-    // Counts are staged through LDS with coalesced loads (up to kScanLds chunks),
-    // each thread scans a contiguous run there, offsets go back coalesced.
-    constexpr int kScanLds = 32768;
-    __shared__ int s_v[kScanLds + 1];
-    __shared__ int s_part[1024];
-    __shared__ int s_total;
+// destination block (dst_start).  A small workgroup with almost no LDS: it
+// must find room on a CU while persistent traces of other pipelines hold
+// nearly every wave slot (a 1024-lane, 130 KB-LDS version waited ~300 us per
+// launch for a drained CU at 16 pipelines).  Tiles of kScanWG x kScanPer
+// counts, each thread a contiguous run of kScanPer, carried across tiles.
+__global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
+    __shared__ int s_part[kScanWG];
+    __shared__ int s_carry;
     const int tid = threadIdx.x;
     const int n = bounce == 0 ? p.npix : p.n_live[bounce];
     const int CH = p.chunk;
     const int nb = (n + CH - 1) / CH;
-    const bool staged = nb <= kScanLds;
-    if (staged)
-        for (int i = tid; i < nb; i += 1024) s_v[i] = p.blk_cnt[i];
+    if (tid == 0) s_carry = 0;
     __syncthreads();
-    const int per = (nb + 1023) / 1024;
-    const int s = tid * per, e = min(s + per, nb);
-    int sum = 0;
-    // explicit branches (not a pointer select): LDS and global reads, no flat loads
-    if (staged) { for (int i = s; i < e; i++) sum += s_v[i]; }
-    else { for (int i = s; i < e; i++) sum += p.blk_cnt[i]; }
-    s_part[tid] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int v = tid >= off ? s_part[tid - off] : 0;
+    for (int base = 0; base < nb; base += kScanWG * kScanPer) {
+        const int i0 = base + tid * kScanPer;
+        int c[kScanPer], sum = 0;
+#pragma unroll
+        for (int q = 0; q < kScanPer; q++) {
+            c[q] = i0 + q < nb ? p.blk_cnt[i0 + q] : 0;
+            sum += c[q];
+        }
+        s_part[tid] = sum;
         __syncthreads();
-        s_part[tid] += v;
+        for (int off = 1; off < kScanWG; off <<= 1) {
+            const int v = tid >= off ? s_part[tid - off] : 0;
+            __syncthreads();
+            s_part[tid] += v;
+            __syncthreads();
+        }
+        const int carry = s_carry;
+        const int tile_total = s_part[kScanWG - 1];
+        int acc = carry + s_part[tid] - sum;        // exclusive
+#pragma unroll
+        for (int q = 0; q < kScanPer; q++) {
+            if (i0 + q >= nb) break;
+            const int o0 = acc, o1 = acc + c[q];
+            p.blk_off[i0 + q] = o0;
+            for (int bd = (o0 + CH - 1) / CH; bd * CH < o1; bd++) p.dst_start[bd] = i0 + q;
+            acc = o1;
+        }
+        __syncthreads();                            // every thread has read s_carry / s_part
+        if (tid == 0) s_carry = carry + tile_total;
         __syncthreads();
-    }
-    int acc = s_part[tid] - sum;   // exclusive
-    if (staged) {
-        for (int i = s; i < e; i++) { const int c = s_v[i]; s_v[i] = acc; acc += c; }
-    } else {
-        for (int i = s; i < e; i++) { const int c = p.blk_cnt[i]; p.blk_off[i] = acc; acc += c; }
-    }
-    if (tid == 1023) {
-        s_total = s_part[1023];
-        p.blk_off[nb] = s_part[1023];
-        p.n_live[bounce + 1] = s_part[1023];
-        atomicAdd(p.segments, (unsigned long long)n);           // shared by concurrent pipelines
-        if (bounce < kMaxBounceCounters) atomicAdd(p.segments + 1 + bounce, (unsigned long long)n);
-    }
-    __syncthreads();
-    if (staged) {
-        s_v[nb] = s_total;
-        for (int i = tid; i < nb; i += 1024) p.blk_off[i] = s_v[i];
-        __syncthreads();
-    }
-    const int total = s_total;
-    for (int i = s; i < e; i++) {
-        int o0, o1;
-        if (staged) { o0 = s_v[i]; o1 = s_v[i + 1]; }
-        else { o0 = p.blk_off[i]; o1 = o0 + p.blk_cnt[i]; }             // this thread's own writes
-        if (o1 == o0) continue;
-        for (int bd = (o0 + CH - 1) / CH; bd * CH < o1; bd++) p.dst_start[bd] = i;
     }
     if (tid == 0) {
+        const int total = s_carry;
+        p.blk_off[nb] = total;
+        p.n_live[bounce + 1] = total;
+        atomicAdd(p.segments, (unsigned long long)n);           // shared by concurrent pipelines
+        if (bounce < kMaxBounceCounters) atomicAdd(p.segments + 1 + bounce, (unsigned long long)n);
         p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
         *p.defer_count = 0;        // and no deferred grid_fast rays
+        *p.cont_count = 0;         // and no drain continuations
+        *p.cont_next = 0;
     }
     if (p.order)                   // empty key histogram and cursors for the next bounce's ray sort
-        for (int i = tid; i < 2 * kSortBins; i += 1024) p.sort_bins[i] = 0;
+        for (int i = tid; i < 2 * kSortBins; i += kScanWG) p.sort_bins[i] = 0;
 }
 
 // Slot map for bounce+1: dense slot blk_off[b] + r <- source index b * chunk + r
@@ -2055,7 +2336,7 @@ __global__ __launch_bounds__(kSortWG) void k_sort_hist(KParams p, int bounce) {
 // position of key b); k_sort_scatter's workgroups reserve their ranges from it.
 __global__ __launch_bounds__(kSortWG) void k_sort_prefix(KParams p) {
     __shared__ int s_part[kSortWG];
-    constexpr int kPerT = kSortBins / kSortWG;           // 4 bins per thread
+    constexpr int kPerT = kSortBins / kSortWG;           // bins per thread
     const int tid = threadIdx.x;
     int v[kPerT], sum = 0;
 #pragma unroll
@@ -2272,6 +2553,11 @@ int Renderer::allocateOnGPU(const Scene& scene) {
             return -1;
         }
         const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (kp.trace_flags & 16));
+        // drain continuations (default variants only: gf flags 9 / 8, bvh flags 11 / 10)
+        const char* dd = std::getenv("PT_DRAIN_DUMP");
+        const bool def_variant = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & ~1) == 8 : (kp.trace_flags & ~1) == 10;
+        kp.drain_dump = split_trace && def_variant ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
+        kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
         kp.spill_stride = spills ? trace_blocks * 64 : 1;
         const char* sm = std::getenv("PT_SLOTMAP");
         kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
@@ -2357,6 +2643,11 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(upload(allocs, &k.trace_next, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.trace_next, 0, sizeof(int), st));
     PT_HIP(upload(allocs, &k.iter_dev, nullptr, sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont, nullptr, (size_t)k.cont_cap * kContFields * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont_count, nullptr, sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont_next, nullptr, sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.cont_count, 0, sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.cont_next, 0, sizeof(int), st));
     return 0;
 }
 
@@ -2393,8 +2684,12 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
                 else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b);
                 break;
         }
+        if (k.drain_dump > 0) {              // the rays handed on in the drain, packed (flags 9 / 8 only)
+            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b);
+            else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b);
+        }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
-        hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, 1024)), t, 0, st, k, b);
+        hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, PT_DEFER_WGS)), t, 0, st, k, b);
         return;
     }
     switch (k.trace_flags & 31) {
@@ -2415,6 +2710,10 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b);
             else hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b);
             break;
+    }
+    if (k.drain_dump > 0) {                  // the rays handed on in the drain, packed (flags 11 / 10 only)
+        if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b);
+        else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b);
     }
 }
 
@@ -2478,7 +2777,7 @@ int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
             e0 = e1 = nullptr;
         }
         if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, k, b);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanWG), 0, st, k, b);
         PT_HIP(hipGetLastError());
         if (k.use_slotmap && b + 1 < passes) {
             hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((k.nblocks * k.chunk + 255) / 256)), dim3(256), 0, st, k, b);

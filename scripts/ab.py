@@ -82,6 +82,10 @@ def main():
             out[v]["deferred"] = allc[77]
             sg = max(rs[v].segments(), 1)
             out[v]["wave_iters_per_segment"] = round(it / sg, 3)
+            # diagnostic slot S lives at segments[S + 64] = allc[S + 63]
+            out[v]["busy_lanes_per_iter"] = round(allc[109] / it, 2)
+            out[v]["drain_iter_share"] = round(allc[107] / it, 3)
+            out[v]["busy_lanes_per_drain_iter"] = round(allc[108] / max(allc[107], 1), 2)
             out[v]["phase_iters_per_segment"] = {k: round(a / sg, 3) for k, (a, b) in ph.items()}
         if "PT_DEBUG_ABLATE=32" in v or "PT_DEBUG_ABLATE=96" in v:   # cycle stamps
             cyc = allc[83:88]
