@@ -84,8 +84,10 @@ struct KParams {
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
     int* cont;                          // drain continuations: rays a persistent trace handed on (SoA, stride cont_cap)
     int cont_cap;
-    int* cont_count;                    // continuation records written (reset by k_scan)
-    int* cont_next;                     // continuation records claimed by the tail launch (reset by k_scan)
+    int* cont_count;                    // [level] records written by that launch (reset by k_scan)
+    int* cont_next;                     // [level] of them claimed by the next tail launch (reset by k_scan)
+    int drain_levels;                   // tail launches after the main one (PT_DRAIN_LEVELS); the last one
+                                        // hands nothing on.  Record buffers alternate between levels
     int drain_dump;                     // hand a wave's rays on once the pool is exhausted and <= this many
                                         // lanes still trace (0: off; PT_DRAIN_DUMP overrides)
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,
@@ -93,6 +95,7 @@ struct KParams {
 };
 
 constexpr int kMaxBounceCounters = 64;
+constexpr int kDrainLevels = 4;          // most tail launches per trace (drain continuations)
 constexpr int kDiagCounters = 64;        // diagnostic counters after the per-bounce ones (PT_TRACE_STATS builds)
 // segments[] slot counting persistent-trace waves that hit trace_iter_cap and left
 // rays untraced (their hit records are stale): any non-zero value invalidates the image

@@ -1177,14 +1177,19 @@ constexpr int kContFields = 57;
 // their own steps, 4 = claim source blocks (else: claim slots + search).
 // TAIL: the tail launch, which resumes drain continuations instead of claiming rays.
 template <int BS, int F, bool TAIL = false>
-__global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, int bounce) {
+__global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, int bounce, int level) {
     static_assert(kCX + 3 + kStack <= kContFields, "continuation record too small");
     __shared__ int s_stack[kStack * BS];
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
     int* stack = s_stack + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
     int* spill = p.spill + sbase;                        // stack entries beyond the LDS part
-    const int ncont = TAIL ? *p.cont_count : 0;
+    // level 0: the main launch; level l >= 1: the tail launch resuming level l - 1's records
+    const size_t cfield = (size_t)p.cont_cap * kContFields;        // one record buffer
+    const int* cin = p.cont + (size_t)((level - 1) & 1) * cfield;   // records this (tail) launch resumes
+    int* cout = p.cont + (size_t)(level & 1) * cfield;              // records it hands on
+    const bool may_dump = level < p.drain_levels;
+    const int ncont = TAIL ? p.cont_count[level - 1] : 0;
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
     // F & 1 is launched only when the scene has at most kLdsModels models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
@@ -1229,13 +1234,13 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 const int cnt = __popcll(idle);
                 const int leader = __ffsll((long long)idle) - 1;
                 int base = 0;
-                if (lane == leader) base = atomicAdd(p.cont_next, cnt);
+                if (lane == leader) base = atomicAdd(p.cont_next + level - 1, cnt);
                 base = __shfl(base, leader);
                 if (base + cnt >= ncont) exhausted = true;
                 if (state == 0) {
                     const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
                     if (r < ncont) {
-                        const int* C = p.cont + r;
+                        const int* C = cin + r;
                         const size_t cs = (size_t)p.cont_cap;
                         j = C[kCJ * cs]; state = C[kCState * cs]; im = C[kCIm * cs];
                         gdist = __int_as_float(C[kCGdist * cs]); gmodel = C[kCGmodel * cs]; gtri = C[kCGtri * cs];
@@ -1333,7 +1338,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             phase = (c2 >= c4 && c2 >= c1) ? 2 : (c4 >= c1 ? 4 : 1);
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
-        if (!TAIL && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
+        if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
             {
@@ -1351,10 +1356,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             const int nbusy = __popcll(bm);
             const int leader = __ffsll((long long)bm) - 1;
             int base = 0;
-            if (lane == leader) base = atomicAdd(p.cont_count, nbusy);
+            if (lane == leader) base = atomicAdd(p.cont_count + level, nbusy);
             base = __shfl(base, leader);
             if (state != 3) {
-                int* C = p.cont + base + __popcll(bm & ((1ull << lane) - 1ull));
+                int* C = cout + base + __popcll(bm & ((1ull << lane) - 1ull));
                 const size_t cs = (size_t)p.cont_cap;
                 C[kCJ * cs] = j; C[kCState * cs] = state; C[kCIm * cs] = im;
                 C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
@@ -1600,7 +1605,7 @@ __device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3
 }
 
 template <int BS, int F, bool TAIL = false>
-__global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce) {
+__global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce, int level) {
     static_assert(kCX + 9 + kGfStack + 4 * kGfHitCap <= kContFields, "continuation record too small");
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
@@ -1609,7 +1614,12 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     int4* hs = s_hs + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
     int* spill = p.spill + sbase;
-    const int ncont = TAIL ? *p.cont_count : 0;
+    // level 0: the main launch; level l >= 1: the tail launch resuming level l - 1's records
+    const size_t cfield = (size_t)p.cont_cap * kContFields;        // one record buffer
+    const int* cin = p.cont + (size_t)((level - 1) & 1) * cfield;   // records this (tail) launch resumes
+    int* cout = p.cont + (size_t)(level & 1) * cfield;              // records it hands on
+    const bool may_dump = level < p.drain_levels;
+    const int ncont = TAIL ? p.cont_count[level - 1] : 0;
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
     // F & 1 is launched only when the scene has at most kLdsModels models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
@@ -1654,13 +1664,13 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
-            if (lane == leader) base = atomicAdd(p.cont_next, cnt);
+            if (lane == leader) base = atomicAdd(p.cont_next + level - 1, cnt);
             base = __shfl(base, leader);
             if (base + cnt >= ncont) exhausted = true;
             if (state == 0) {
                 const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (r < ncont) {
-                    const int* C = p.cont + r;
+                    const int* C = cin + r;
                     const size_t cs = (size_t)p.cont_cap;
                     j = C[kCJ * cs]; state = C[kCState * cs]; im = C[kCIm * cs];
                     gdist = __int_as_float(C[kCGdist * cs]); gmodel = C[kCGmodel * cs]; gtri = C[kCGtri * cs];
@@ -1768,7 +1778,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (c1 > cm) { phase = 1; cm = c1; }
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
-        if (!TAIL && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
+        if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
             {
@@ -1788,10 +1798,10 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int nbusy = __popcll(bm);
             const int leader = __ffsll((long long)bm) - 1;
             int base = 0;
-            if (lane == leader) base = atomicAdd(p.cont_count, nbusy);
+            if (lane == leader) base = atomicAdd(p.cont_count + level, nbusy);
             base = __shfl(base, leader);
             if (state != 3) {
-                int* C = p.cont + base + __popcll(bm & ((1ull << lane) - 1ull));
+                int* C = cout + base + __popcll(bm & ((1ull << lane) - 1ull));
                 const size_t cs = (size_t)p.cont_cap;
                 C[kCJ * cs] = j; C[kCState * cs] = state; C[kCIm * cs] = im;
                 C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
@@ -2226,8 +2236,10 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
         *p.defer_count = 0;        // and no deferred grid_fast rays
-        *p.cont_count = 0;         // and no drain continuations
-        *p.cont_next = 0;
+        for (int l = 0; l < kDrainLevels; l++) {   // and no drain continuations
+            p.cont_count[l] = 0;
+            p.cont_next[l] = 0;
+        }
     }
     if (p.order)                   // empty key histogram and cursors for the next bounce's ray sort
         for (int i = tid; i < 2 * kSortBins; i += kScanWG) p.sort_bins[i] = 0;
@@ -2558,6 +2570,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const bool def_variant = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & ~1) == 8 : (kp.trace_flags & ~1) == 10;
         kp.drain_dump = split_trace && def_variant ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
+        const char* dl = std::getenv("PT_DRAIN_LEVELS");     // tail launches; the last one runs to the end
+        kp.drain_levels = std::max(1, std::min(kDrainLevels, dl ? std::atoi(dl) : 1));
         kp.spill_stride = spills ? trace_blocks * 64 : 1;
         const char* sm = std::getenv("PT_SLOTMAP");
         kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
@@ -2643,11 +2657,11 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(upload(allocs, &k.trace_next, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.trace_next, 0, sizeof(int), st));
     PT_HIP(upload(allocs, &k.iter_dev, nullptr, sizeof(int), st));
-    PT_HIP(upload(allocs, &k.cont, nullptr, (size_t)k.cont_cap * kContFields * sizeof(int), st));
-    PT_HIP(upload(allocs, &k.cont_count, nullptr, sizeof(int), st));
-    PT_HIP(upload(allocs, &k.cont_next, nullptr, sizeof(int), st));
-    PT_HIP(hipMemsetAsync(k.cont_count, 0, sizeof(int), st));
-    PT_HIP(hipMemsetAsync(k.cont_next, 0, sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont, nullptr, 2 * (size_t)k.cont_cap * kContFields * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont_count, nullptr, kDrainLevels * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont_next, nullptr, kDrainLevels * sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.cont_count, 0, kDrainLevels * sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.cont_next, 0, kDrainLevels * sizeof(int), st));
     return 0;
 }
 
@@ -2674,46 +2688,46 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
         switch (gf_flags) {
-            case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b); break;
-            case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b); break;
-            case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b); break;
-            case 12: hipLaunchKernelGGL((k_trace_gf<64, 12>), g, t, 0, st, k, b); break;
-            case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b); break;
+            case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b, 0); break;
+            case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b, 0); break;
+            case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0); break;
+            case 12: hipLaunchKernelGGL((k_trace_gf<64, 12>), g, t, 0, st, k, b, 0); break;
+            case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b, 0); break;
             default:                         // 9; 8 when the model records do not fit LDS
-                if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b);
-                else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b);
+                if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
+                else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
                 break;
         }
-        if (k.drain_dump > 0) {              // the rays handed on in the drain, packed (flags 9 / 8 only)
-            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b);
-            else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b);
+        for (int l = 1; k.drain_dump > 0 && l <= k.drain_levels; l++) {   // the rays handed on, packed
+            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b, l);
+            else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b, l);
         }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
         hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, PT_DEFER_WGS)), t, 0, st, k, b);
         return;
     }
     switch (k.trace_flags & 31) {
-        case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, st, k, b); break;
-        case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, st, k, b); break;
-        case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, st, k, b); break;
-        case 3: hipLaunchKernelGGL((k_trace_bvh<64, 3>), g, t, 0, st, k, b); break;
-        case 4: hipLaunchKernelGGL((k_trace_bvh<64, 4>), g, t, 0, st, k, b); break;
-        case 5: hipLaunchKernelGGL((k_trace_bvh<64, 5>), g, t, 0, st, k, b); break;
-        case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, st, k, b); break;
-        case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, st, k, b); break;
-        case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b); break;
-        case 26: hipLaunchKernelGGL((k_trace_bvh<64, 26>), g, t, 0, st, k, b); break;
-        case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, st, k, b); break;
-        case 18: hipLaunchKernelGGL((k_trace_bvh<64, 18>), g, t, 0, st, k, b); break;
-        case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, st, k, b); break;
+        case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, st, k, b, 0); break;
+        case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, st, k, b, 0); break;
+        case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, st, k, b, 0); break;
+        case 3: hipLaunchKernelGGL((k_trace_bvh<64, 3>), g, t, 0, st, k, b, 0); break;
+        case 4: hipLaunchKernelGGL((k_trace_bvh<64, 4>), g, t, 0, st, k, b, 0); break;
+        case 5: hipLaunchKernelGGL((k_trace_bvh<64, 5>), g, t, 0, st, k, b, 0); break;
+        case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, st, k, b, 0); break;
+        case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, st, k, b, 0); break;
+        case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b, 0); break;
+        case 26: hipLaunchKernelGGL((k_trace_bvh<64, 26>), g, t, 0, st, k, b, 0); break;
+        case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, st, k, b, 0); break;
+        case 18: hipLaunchKernelGGL((k_trace_bvh<64, 18>), g, t, 0, st, k, b, 0); break;
+        case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, st, k, b, 0); break;
         default:                             // 11; 10 when the model records do not fit LDS
-            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b);
-            else hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b);
+            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b, 0);
+            else hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b, 0);
             break;
     }
-    if (k.drain_dump > 0) {                  // the rays handed on in the drain, packed (flags 11 / 10 only)
-        if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b);
-        else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b);
+    for (int l = 1; k.drain_dump > 0 && l <= k.drain_levels; l++) {       // the rays handed on, packed
+        if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b, l);
+        else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b, l);
     }
 }
 

@@ -456,9 +456,9 @@ def test_graph_replay_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypa
 
 
 @pytest.mark.parametrize("accel", [1, 2])
-@pytest.mark.parametrize("dump", [0, 1, 32, 64])
+@pytest.mark.parametrize("dump,levels", [(0, 1), (1, 1), (32, 1), (64, 1), (32, 4), (64, 2)])
 @pytest.mark.parametrize("scene", ["synthetic", "reference"])
-def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, dump, scene):
+def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, dump, levels, scene):
     """PT_DRAIN_DUMP: waves of a persistent trace whose pool is exhausted hand
     their last <= dump rays (exact traversal state: stack, hit set, pending
     leaves) to a tail launch.  Images and segment counts stay the oracle's for
@@ -467,10 +467,11 @@ def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, mo
     from pathtracerap_amd import synthetic
     P, O = pt_mod, oracle_mod
     monkeypatch.setenv("PT_DRAIN_DUMP", str(dump))
+    monkeypatch.setenv("PT_DRAIN_LEVELS", str(levels))   # tail launches; all but the last hand on again
     path = synthetic.diffuse_scene(synth_dir, ntri=6000, seed=13, metallic=True) if scene == "synthetic" else REF_SCENE
     s = P.Scene(path)
     s.build(bvh=True)
     cfg = P.RenderConfig(width=211, height=97, iterations=3, max_bounces=7, accel=accel, pipelines=4)
     img, seg, oimg, oseg = _render_both(P, O, s, cfg)
     assert seg == oseg
-    assert_bitexact(img, oimg, f"PT_DRAIN_DUMP={dump} {scene}")
+    assert_bitexact(img, oimg, f"PT_DRAIN_DUMP={dump} PT_DRAIN_LEVELS={levels} {scene}")
