@@ -2598,6 +2598,14 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* pe = std::getenv("PT_PIPES");
         npipes = std::max(1, std::min(kMaxPipes, pe ? std::atoi(pe) : cfg.pipelines));
     }
+    // Drain continuations pay off only when other pipelines' kernels take the
+    // wave slots a draining trace frees: with one pipeline they only add the
+    // hand-on and the tail launch (measured 0.76 -> 0.91 ms per trace), so
+    // they stay off there unless PT_DRAIN_DUMP asks for them.
+    if (npipes == 1 && !std::getenv("PT_DRAIN_DUMP")) {
+        kp.drain_dump = 0;
+        kp.cont_cap = 1;
+    }
     kp.contrib = nullptr;
     pstream[0] = stream;
     for (int i = 1; i < npipes; i++) {
