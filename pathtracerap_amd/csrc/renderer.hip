@@ -1151,7 +1151,7 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 }
 
 #ifndef PT_BVH_MINWAVES
-#define PT_BVH_MINWAVES 1     // waves per SIMD the k_trace_bvh register allocation must allow (5 spills 3 VGPRs, no faster)
+#define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
 #endif
 constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
 constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
@@ -2498,6 +2498,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         PT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         own_stream = true;
     }
+    {
+        const char* pe = std::getenv("PT_PIPES");
+        npipes = std::max(1, std::min(kMaxPipes, pe ? std::atoi(pe) : cfg.pipelines));
+    }
     kp = KParams{};
     kp.nmodels = (int)scene.model_recs.size();
     for (int k = 0; k < 3; k++) kp.gdim[k] = scene.grid_dim[k];
@@ -2556,8 +2560,14 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         if (scene.model_recs.size() > (size_t)kLdsModels) kp.trace_flags &= ~1;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        // Waves per CU of a persistent trace launch: with one pipeline the launch
+        // fills the chip alone (20; k_trace_gf keeps 16 resident); with several,
+        // 8 per launch lets 2-3 pipelines' traces share the CUs, so one launch's
+        // drain overlaps another's full waves (measured at 16 pipelines: 20 ->
+        // 8 waves 2141 -> 2256 Mrays/s grid_fast, 3211 -> 3393 bvh; 4 / 6 / 10 /
+        // 12 / 16 / 32: 2180 / 2232 / 2245 / 2190 / 2188 / 2034).
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
-        const int w = wpc ? std::max(1, std::atoi(wpc)) : 20;   // resident waves per CU
+        const int w = wpc ? std::max(1, std::atoi(wpc)) : (npipes > 1 ? 8 : 20);
         trace_blocks = std::max(1, cus) * w;
         // 4-wide traversal pushes up to 3 entries per level: LDS holds kStack, the rest spills
         if (split_trace && (kp.trace_flags & 16) && 3 * scene.bvh4_max_depth > kStack + kSpillEntries) {
@@ -2593,11 +2603,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.segments, nullptr, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.segments, 0, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     // Pipelines: iterations in flight on their own streams, each with its own
-    // ray pools, scan state, hit buffer and work counters (PT_PIPES overrides).
-    {
-        const char* pe = std::getenv("PT_PIPES");
-        npipes = std::max(1, std::min(kMaxPipes, pe ? std::atoi(pe) : cfg.pipelines));
-    }
+    // ray pools, scan state, hit buffer and work counters (npipes: set above).
     // Drain continuations pay off only when other pipelines' kernels take the
     // wave slots a draining trace frees: with one pipeline they only add the
     // hand-on and the tail launch (measured 0.76 -> 0.91 ms per trace), so
