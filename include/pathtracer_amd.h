@@ -66,7 +66,7 @@ typedef struct pt_render_config {
     int block;                /* bounce-kernel workgroup = compaction chunk: 64 (default), 128 or 256 */
     int pipelines;            /* iterations in flight on their own HIP streams, 1..16 (default 8); results
                                  are identical for every value (contributions merge in iteration order) */
-    int ray_sort;             /* ray sort before each persistent trace: -1 auto (grid_fast: key 7, bvh: off),
+    int ray_sort;             /* ray sort before each persistent trace: -1 auto (key 7 for grid_fast and bvh),
                                  0 off, 1..8 key layout; claim order only, results identical */
 } pt_render_config;
 
