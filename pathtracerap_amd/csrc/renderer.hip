@@ -1639,8 +1639,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     // lane state: 0 needs a ray, 1 select model, 2 node visit, 4 leaf triangle, 5 walk, 3 no more rays
     int state = 0;
     int j = -1;
-    f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0), winv = mk3(0, 0, 0);
-    float dlen = 0.0f, gdist = kFMax;
+    f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0);
+    float gdist = kFMax;
     int gmodel = -1, gtri = -1, im = -1;
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0), G = mk3(0, 0, 0);
     float t_box = 0.0f, tmin = kFMax, win = 0.0f;
@@ -1694,8 +1694,6 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                     for (int q = 0; q < kGfHitCap; q++)
                         hs[q * BS] = make_int4(C[(kCX + 9 + kGfStack + 4 * q) * cs], C[(kCX + 10 + kGfStack + 4 * q) * cs],
                                                C[(kCX + 11 + kGfStack + 4 * q) * cs], C[(kCX + 12 + kGfStack + 4 * q) * cs]);
-                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
-                    dlen = sqrtf(dot(dw, dw));
                     if (state != 1) {                       // inside model im: its model-space ray, as selected
                         const ModelRec& M = models[im];
                         o = xform12(M.w2m, ow, 1.0f);
@@ -1728,8 +1726,6 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                     const float4 b = p.ray[in_buf][1][src];
                     ow = mk3(a.x, a.y, a.z);
                     dw = mk3(b.x, b.y, b.z);
-                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
-                    dlen = sqrtf(dot(dw, dw));
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
                     state = 1;
                 }
@@ -1753,8 +1749,6 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                     const float4 b = p.ray[in_buf][1][src];
                     ow = mk3(a.x, a.y, a.z);
                     dw = mk3(b.x, b.y, b.z);
-                    winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
-                    dlen = sqrtf(dot(dw, dw));
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
                     state = 1;
                 } else {
@@ -1829,6 +1823,10 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             state = 3;
         }
         if ((phase & 1) && state == 1) {                // next model that survives culling and the grid entry test
+            // world-space slopes for the instance culling: recomputed here (select steps are
+            // rare) instead of living in registers through the traversal
+            const f3 winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+            const float dlen = sqrtf(dot(dw, dw));
             for (;;) {
                 im++;
                 if (im >= p.nmodels) {
