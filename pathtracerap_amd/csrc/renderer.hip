@@ -1150,6 +1150,9 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
     return n;
 }
 
+#ifndef PT_LEAF_STEP
+#define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of the persistent traces (1 or 2)
+#endif
 #ifndef PT_BVH_MINWAVES
 #define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
 #endif
@@ -1409,13 +1412,28 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             }
         }
         bool model_done = false;
-        if ((phase & 4) && state == 4) {                // one leaf triangle per iteration
+        if ((phase & 4) && state == 4) {                // leaf triangles: up to PT_LEAF_STEP per iteration
+            // the step's triangle loads are issued together (one memory round trip);
+            // the (t, index) minimum does not depend on the order of the tests
+            const int i1 = (PT_LEAF_STEP > 1 && lf_i + 1 < lf_e) ? lf_i + 1 : lf_i;
             const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
-            const int it = __float_as_int(A.w);
-            float t;
-            if (tri_test_rec(A, B, C, o, d, t)) {
-                any = true;
-                if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+            const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
+            {
+                const int it = __float_as_int(A.w);
+                float t;
+                if (tri_test_rec(A, B, C, o, d, t)) {
+                    any = true;
+                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+                }
+            }
+            if (i1 != lf_i) {
+                const int it = __float_as_int(A1.w);
+                float t;
+                if (tri_test_rec(A1, B1, C1, o, d, t)) {
+                    any = true;
+                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+                }
+                lf_i++;
             }
             lf_i++;
             if ((F & 16) && lf_i == lf_e) {             // 4-wide: everything pending is on the stack
@@ -1866,71 +1884,79 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         }
         if (stamps) { const unsigned long long t = clock64(); cy[1] += t - ts; ts = t; }
         bool collected = false;
-        if ((phase & 4) && state == 4) {                // one leaf triangle of the collection
-            const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
-            float t;
-            if (tri_test_rec(A, B, C, o, d, t)) {
-                if (t < tmin) tmin = t;
-                const ModelRec& M = models[im];
-                const float X = tmin + win;
-                const float Xs = X + gf_slack(X, t_box);
-                if (!(vbox_entry(M, __float_as_int(B.w), __float_as_int(C.w), o, ninv) > Xs)) {   // required member
-                    const int4 e = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
-                                             __float_as_int(C.w));
-                    if (pblk < 0) {
-                        if (nh == kGfHitCap) {          // drop members now beyond the bound
-                            int wn = 0;
-                            for (int q = 0; q < nh; q++) {
-                                const int4 x = hs[q * BS];
-                                if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) hs[(wn++) * BS] = x;
+        if ((phase & 4) && state == 4) {                // leaf triangles of the collection: up to PT_LEAF_STEP
+            // per step, their loads issued together; tested in leaf order, as one per step would
+            const int i1 = (PT_LEAF_STEP > 1 && lf_i + 1 < lf_e) ? lf_i + 1 : lf_i;
+            const float4 A0 = p.bvh_tri_geom[3 * lf_i], B0 = p.bvh_tri_geom[3 * lf_i + 1], C0 = p.bvh_tri_geom[3 * lf_i + 2];
+            const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
+            const int n_step = i1 != lf_i ? 2 : 1;
+#pragma unroll 1
+            for (int k = 0; k < n_step && state == 4; k++) {
+                const float4 A = k ? A1 : A0, B = k ? B1 : B0, C = k ? C1 : C0;
+                float t;
+                if (tri_test_rec(A, B, C, o, d, t)) {
+                    if (t < tmin) tmin = t;
+                    const ModelRec& M = models[im];
+                    const float X = tmin + win;
+                    const float Xs = X + gf_slack(X, t_box);
+                    if (!(vbox_entry(M, __float_as_int(B.w), __float_as_int(C.w), o, ninv) > Xs)) {   // required member
+                        const int4 e = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
+                                                 __float_as_int(C.w));
+                        if (pblk < 0) {
+                            if (nh == kGfHitCap) {          // drop members now beyond the bound
+                                int wn = 0;
+                                for (int q = 0; q < nh; q++) {
+                                    const int4 x = hs[q * BS];
+                                    if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) hs[(wn++) * BS] = x;
+                                }
+                                nh = wn;
                             }
-                            nh = wn;
-                        }
-                        if (nh == kGfHitCap) {          // LDS full: continue in a 64-member global pool block
-                            const int blk = atomicAdd(p.hs_pool_next, 1);
-                            if (blk < p.hs_pool_blocks) {
-                                pblk = blk;
-                                int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
-                                for (int q = 0; q < nh; q++) g[q] = hs[q * BS];
+                            if (nh == kGfHitCap) {          // LDS full: continue in a 64-member global pool block
+                                const int blk = atomicAdd(p.hs_pool_next, 1);
+                                if (blk < p.hs_pool_blocks) {
+                                    pblk = blk;
+                                    int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
+                                    for (int q = 0; q < nh; q++) g[q] = hs[q * BS];
+                                }
                             }
                         }
-                    }
-                    if (pblk >= 0) {
-                        int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
-                        if (nh == kHitCapPool) {
-                            int wn = 0;
-                            for (int q = 0; q < nh; q++) {
-                                const int4 x = g[q];
-                                if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) g[wn++] = x;
+                        if (pblk >= 0) {
+                            int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
+                            if (nh == kHitCapPool) {
+                                int wn = 0;
+                                for (int q = 0; q < nh; q++) {
+                                    const int4 x = g[q];
+                                    if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) g[wn++] = x;
+                                }
+                                nh = wn;
                             }
-                            nh = wn;
+                            if (nh < kHitCapPool) g[nh++] = e;
+                            else { p.defer_slots[atomicAdd(p.defer_count, 1)] = j; state = 0; }   // pool block full too
+                        } else if (nh < kGfHitCap) {
+                            hs[nh * BS] = e;
+                            nh++;
+                        } else {                            // pool exhausted: the whole ray goes to k_trace_deferred
+                            p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                            state = 0;
                         }
-                        if (nh < kHitCapPool) g[nh++] = e;
-                        else { p.defer_slots[atomicAdd(p.defer_count, 1)] = j; state = 0; }   // pool block full too
-                    } else if (nh < kGfHitCap) {
-                        hs[nh * BS] = e;
-                        nh++;
-                    } else {                            // pool exhausted: the whole ray goes to k_trace_deferred
-                        p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
-                        state = 0;
                     }
                 }
-            }
-            if (state == 4) {
-                lf_i++;
-                if (lf_i == lf_e) {
-                    if (lf2_i < lf2_e) {
-                        lf_i = lf2_i; lf_e = lf2_e;
-                        lf2_i = lf2_e = 0;
-                    } else if (lf_next >= 0) {
-                        cur = lf_next;
-                        state = 2;
-                    } else if (sp == 0) {
-                        collected = true;
-                    } else {
-                        sp--;
-                        cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
-                        state = 2;
+                if (state == 4) {
+                    lf_i++;
+                    if (lf_i == lf_e) {
+                        if (lf2_i < lf2_e) {
+                            lf_i = lf2_i; lf_e = lf2_e;
+                            lf2_i = lf2_e = 0;
+                        } else if (lf_next >= 0) {
+                            cur = lf_next;
+                            state = 2;
+                        } else if (sp == 0) {
+                            collected = true;
+                        } else {
+                            sp--;
+                            cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
+                            state = 2;
+                        }
                     }
                 }
             }
