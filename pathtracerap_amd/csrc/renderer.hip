@@ -1151,7 +1151,7 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 }
 
 #ifndef PT_LEAF_STEP
-#define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of the persistent traces (1 or 2)
+#define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of k_trace_bvh (1..4; k_trace_gf: 1 or 2)
 #endif
 #ifndef PT_BVH_MINWAVES
 #define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
@@ -1415,27 +1415,23 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
         if ((phase & 4) && state == 4) {                // leaf triangles: up to PT_LEAF_STEP per iteration
             // the step's triangle loads are issued together (one memory round trip);
             // the (t, index) minimum does not depend on the order of the tests
-            const int i1 = (PT_LEAF_STEP > 1 && lf_i + 1 < lf_e) ? lf_i + 1 : lf_i;
-            const float4 A = p.bvh_tri_geom[3 * lf_i], B = p.bvh_tri_geom[3 * lf_i + 1], C = p.bvh_tri_geom[3 * lf_i + 2];
-            const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
-            {
-                const int it = __float_as_int(A.w);
+            float4 TA[PT_LEAF_STEP], TB[PT_LEAF_STEP], TC[PT_LEAF_STEP];
+#pragma unroll
+            for (int q = 0; q < PT_LEAF_STEP; q++) {
+                const int iq = lf_i + q < lf_e ? lf_i + q : lf_i;
+                TA[q] = p.bvh_tri_geom[3 * iq]; TB[q] = p.bvh_tri_geom[3 * iq + 1]; TC[q] = p.bvh_tri_geom[3 * iq + 2];
+            }
+#pragma unroll
+            for (int q = 0; q < PT_LEAF_STEP; q++) {
+                if (lf_i + q >= lf_e) break;
+                const int it = __float_as_int(TA[q].w);
                 float t;
-                if (tri_test_rec(A, B, C, o, d, t)) {
+                if (tri_test_rec(TA[q], TB[q], TC[q], o, d, t)) {
                     any = true;
                     if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
                 }
             }
-            if (i1 != lf_i) {
-                const int it = __float_as_int(A1.w);
-                float t;
-                if (tri_test_rec(A1, B1, C1, o, d, t)) {
-                    any = true;
-                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
-                }
-                lf_i++;
-            }
-            lf_i++;
+            lf_i = min(lf_i + PT_LEAF_STEP, lf_e);
             if ((F & 16) && lf_i == lf_e) {             // 4-wide: everything pending is on the stack
                 if (sp == 0) {
                     model_done = true;
@@ -1886,6 +1882,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         bool collected = false;
         if ((phase & 4) && state == 4) {                // leaf triangles of the collection: up to PT_LEAF_STEP
             // per step, their loads issued together; tested in leaf order, as one per step would
+            // (k_trace_gf: at most two -- selecting from a longer array spilled 33+ VGPRs)
             const int i1 = (PT_LEAF_STEP > 1 && lf_i + 1 < lf_e) ? lf_i + 1 : lf_i;
             const float4 A0 = p.bvh_tri_geom[3 * lf_i], B0 = p.bvh_tri_geom[3 * lf_i + 1], C0 = p.bvh_tri_geom[3 * lf_i + 2];
             const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
