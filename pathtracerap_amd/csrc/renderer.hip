@@ -2598,7 +2598,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (kp.trace_flags & 16));
         // drain continuations (default variants only: gf flags 9 / 8, bvh flags 11 / 10)
         const char* dd = std::getenv("PT_DRAIN_DUMP");
-        const bool def_variant = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & ~1) == 8 : (kp.trace_flags & ~1) == 10;
+        const bool def_variant = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & ~1) == 8
+                                                              : ((kp.trace_flags & ~1) == 10 || (kp.trace_flags & ~1) == 26);
         kp.drain_dump = split_trace && def_variant ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
         const char* dl = std::getenv("PT_DRAIN_LEVELS");     // tail launches; the last one runs to the end
@@ -2761,9 +2762,15 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             else hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b, 0);
             break;
     }
+    const bool wide = (k.trace_flags & 16) != 0;
     for (int l = 1; k.drain_dump > 0 && l <= k.drain_levels; l++) {       // the rays handed on, packed
-        if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b, l);
-        else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b, l);
+        if (wide) {
+            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 27, true>), g, t, 0, st, k, b, l);
+            else hipLaunchKernelGGL((k_trace_bvh<64, 26, true>), g, t, 0, st, k, b, l);
+        } else {
+            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b, l);
+            else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b, l);
+        }
     }
 }
 
