@@ -1153,6 +1153,12 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 #ifndef PT_LEAF_STEP
 #define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of k_trace_bvh (1..4; k_trace_gf: 1 or 2)
 #endif
+#ifndef PT_BVH_LEAF_W
+#define PT_BVH_LEAF_W 4       // k_trace_bvh phase weights (x/4) of leaf and select lane counts against node's
+#endif
+#ifndef PT_BVH_SEL_W
+#define PT_BVH_SEL_W 4
+#endif
 #ifndef PT_BVH_MINWAVES
 #define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
 #endif
@@ -1338,7 +1344,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
         if (F & 8) {
             const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
                       c4 = __popcll(__ballot(state == 4));
-            phase = (c2 >= c4 && c2 >= c1) ? 2 : (c4 >= c1 ? 4 : 1);
+            phase = 2; int cm = c2;
+            if (c4 * 4 > cm * PT_BVH_LEAF_W) { phase = 4; cm = c4; }
+            if (c1 * 4 > cm * PT_BVH_SEL_W) phase = 1;
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
@@ -1574,6 +1582,15 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_HITCAP
 #define PT_GF_HITCAP 4
 #endif
+#ifndef PT_WALK_W
+#define PT_WALK_W 8           // k_trace_gf: the walk phase runs when its lanes outnumber the largest other phase's x W/4
+#endif
+#ifndef PT_LEAF_W
+#define PT_LEAF_W 3           // ... and the leaf phase when they exceed node's x 3/4 (select: x PT_SEL_W/4)
+#endif
+#ifndef PT_SEL_W
+#define PT_SEL_W 4
+#endif
 #ifndef PT_GF_MINWAVES
 #define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
 #endif
@@ -1781,9 +1798,9 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
                       c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5));
             phase = 2; int cm = c2;
-            if (c4 > cm) { phase = 4; cm = c4; }
-            if (c5 > cm) { phase = 8; cm = c5; }
-            if (c1 > cm) { phase = 1; cm = c1; }
+            if (c4 * 4 > cm * PT_LEAF_W) { phase = 4; cm = c4; }
+            if (c5 * 4 > cm * PT_WALK_W) { phase = 8; cm = c5; }
+            if (c1 * 4 > cm * PT_SEL_W) { phase = 1; cm = c1; }
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
