@@ -1585,6 +1585,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_WALK_W
 #define PT_WALK_W 8           // k_trace_gf: the walk phase runs when its lanes outnumber the largest other phase's x W/4
 #endif
+#ifndef PT_WALK_DEFER
+#define PT_WALK_DEFER 1       // k_trace_gf: a walk the certificate cannot decide defers its ray to k_trace_deferred
+#endif
 #ifndef PT_LEAF_W
 #define PT_LEAF_W 3           // ... and the leaf phase when they exceed node's x 3/4 (select: x PT_SEL_W/4)
 #endif
@@ -2044,12 +2047,26 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (PT_TRACE_STATS && (p.debug & 128) && pblk < 0) {      // timing-only ablation: no walk at all
                 w.hit = true; w.has_best = true; w.final_min = true; w.t = tmin; w.tri = -1; w.tw = 0.0f;
                 for (int h = 0; h < nh; h++) if (__int_as_float(hs[h * BS].x) == tmin) w.tri = hs[h * BS].y;
+            } else if (PT_WALK_DEFER) {
+                // the certificate only; a ray it cannot decide goes whole to k_trace_deferred
+                int tri = -1;
+                const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
+                const bool ok = pblk < 0
+                    ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
+                    : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
+                w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
+                if (!ok) {
+                    p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                    state = 0;
+                }
             } else {
                 w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
                              : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
                                                     tmin, win);
             }
-            if (tier == 2 || w.final_min || w.tw < tmin + win) {
+            if (state == 0) {
+                // deferred
+            } else if (tier == 2 || w.final_min || w.tw < tmin + win) {
                 if (w.hit && w.has_best) {
                     const float dd = model_hit_dist(M, o, d, w.t, ow);
                     if (gdist > dd) { gdist = dd; gmodel = im; gtri = w.tri; }
