@@ -84,7 +84,9 @@ struct KParams {
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
     int* cont;                          // drain continuations: rays a persistent trace handed on (SoA, stride cont_cap)
     int cont_cap;
-    int* cont_count;                    // [level] records written by that launch (reset by k_scan)
+    int* cont_count;                    // [level] records written by that launch, [kDrainLevels + level]
+                                        // walk hand-ons it wrote (k_trace_gf; reset by k_scan)
+    int cont_wcap;                      // walk hand-on records per launch (at the top of the buffer; 0: off)
     int* cont_next;                     // [level] of them claimed by the next tail launch (reset by k_scan)
     int drain_levels;                   // tail launches after the main one (PT_DRAIN_LEVELS); the last one
                                         // hands nothing on.  Record buffers alternate between levels

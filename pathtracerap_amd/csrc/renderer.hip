@@ -1653,7 +1653,9 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     const int* cin = p.cont + (size_t)((level - 1) & 1) * cfield;   // records this (tail) launch resumes
     int* cout = p.cont + (size_t)(level & 1) * cfield;              // records it hands on
     const bool may_dump = level < p.drain_levels;
-    const int ncont = TAIL ? p.cont_count[level - 1] : 0;
+    // records: drain hand-ons at [0, nd), walk hand-ons (level 1 only) at [cont_cap - nw, cont_cap)
+    const int nd = TAIL ? p.cont_count[level - 1] : 0;
+    const int ncont = nd + (TAIL && level == 1 ? min(p.cont_count[kDrainLevels], p.cont_wcap) : 0);
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
     // F & 1 is launched only when the scene has at most kLdsModels models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
@@ -1704,7 +1706,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (state == 0) {
                 const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (r < ncont) {
-                    const int* C = cin + r;
+                    const int* C = cin + (r < nd ? r : p.cont_cap - 1 - (r - nd));
                     const size_t cs = (size_t)p.cont_cap;
                     j = C[kCJ * cs]; state = C[kCState * cs]; im = C[kCIm * cs];
                     gdist = __int_as_float(C[kCGdist * cs]); gmodel = C[kCGmodel * cs]; gtri = C[kCGtri * cs];
@@ -1716,6 +1718,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                     lf_i = C[kCLfI * cs]; lf_e = C[kCLfE * cs]; lf2_i = C[kCLf2I * cs]; lf2_e = C[kCLf2E * cs];
                     lf_next = C[kCLfNext * cs];
                     sbase = C[kCSpill * cs];
+                    // a walk hand-on's traversal stack is empty: this lane's own tail area
+                    if (sbase < 0) sbase = p.spill_stride / 2 + (int)(blockIdx.x * BS + threadIdx.x);
                     spill = p.spill + sbase;
                     tmin = __int_as_float(C[kCX * cs]); nh = C[(kCX + 1) * cs]; tier = C[(kCX + 2) * cs];
                     pblk = C[(kCX + 3) * cs]; win = __int_as_float(C[(kCX + 4) * cs]);
@@ -1820,42 +1824,6 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[0] += t - ts; ts = t; }
-        if (phase & 16) {
-            // drain continuation: every busy lane's exact state, then the wave is done
-            const unsigned long long bm = __ballot(state != 3);
-            const int nbusy = __popcll(bm);
-            const int leader = __ffsll((long long)bm) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(p.cont_count + level, nbusy);
-            base = __shfl(base, leader);
-            if (state != 3) {
-                int* C = cout + base + __popcll(bm & ((1ull << lane) - 1ull));
-                const size_t cs = (size_t)p.cont_cap;
-                C[kCJ * cs] = j; C[kCState * cs] = state; C[kCIm * cs] = im;
-                C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
-                C[kCOw * cs] = __float_as_int(ow.x); C[(kCOw + 1) * cs] = __float_as_int(ow.y);
-                C[(kCOw + 2) * cs] = __float_as_int(ow.z);
-                C[kCDw * cs] = __float_as_int(dw.x); C[(kCDw + 1) * cs] = __float_as_int(dw.y);
-                C[(kCDw + 2) * cs] = __float_as_int(dw.z);
-                C[kCCur * cs] = cur; C[kCSp * cs] = sp;
-                C[kCLfI * cs] = lf_i; C[kCLfE * cs] = lf_e; C[kCLf2I * cs] = lf2_i; C[kCLf2E * cs] = lf2_e;
-                C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = sbase;
-                C[kCX * cs] = __float_as_int(tmin); C[(kCX + 1) * cs] = nh; C[(kCX + 2) * cs] = tier;
-                C[(kCX + 3) * cs] = pblk; C[(kCX + 4) * cs] = __float_as_int(win);
-                C[(kCX + 5) * cs] = __float_as_int(t_box);
-                C[(kCX + 6) * cs] = __float_as_int(G.x); C[(kCX + 7) * cs] = __float_as_int(G.y);
-                C[(kCX + 8) * cs] = __float_as_int(G.z);
-#pragma unroll 1
-                for (int q = 0; q < kGfStack; q++) C[(kCX + 9 + q) * cs] = stack[q * BS];
-#pragma unroll 1
-                for (int q = 0; q < kGfHitCap; q++) {
-                    const int4 e = hs[q * BS];
-                    C[(kCX + 9 + kGfStack + 4 * q) * cs] = e.x; C[(kCX + 10 + kGfStack + 4 * q) * cs] = e.y;
-                    C[(kCX + 11 + kGfStack + 4 * q) * cs] = e.z; C[(kCX + 12 + kGfStack + 4 * q) * cs] = e.w;
-                }
-            }
-            state = 3;
-        }
         if ((phase & 1) && state == 1) {                // next model that survives culling and the grid entry test
             // world-space slopes for the instance culling: recomputed here (select steps are
             // rare) instead of living in registers through the traversal
@@ -2047,25 +2015,23 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (PT_TRACE_STATS && (p.debug & 128) && pblk < 0) {      // timing-only ablation: no walk at all
                 w.hit = true; w.has_best = true; w.final_min = true; w.t = tmin; w.tri = -1; w.tw = 0.0f;
                 for (int h = 0; h < nh; h++) if (__int_as_float(hs[h * BS].x) == tmin) w.tri = hs[h * BS].y;
-            } else if (PT_WALK_DEFER) {
-                // the certificate only; a ray it cannot decide goes whole to k_trace_deferred
+            } else if (!TAIL && PT_WALK_DEFER) {
+                // the certificate only; a ray it cannot decide is handed on to the tail launch
+                // (which walks it exactly) or, past the records' room, to k_trace_deferred
                 int tri = -1;
                 const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
                 const bool ok = pblk < 0
                     ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
                     : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
-                if (!ok) {
-                    p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
-                    state = 0;
-                }
+                if (!ok) state = 6;
             } else {
                 w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
                              : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
                                                     tmin, win);
             }
-            if (state == 0) {
-                // deferred
+            if (state == 6) {
+                // handed on below
             } else if (tier == 2 || w.final_min || w.tw < tmin + win) {
                 if (w.hit && w.has_best) {
                     const float dd = model_hit_dist(M, o, d, w.t, ow);
@@ -2079,6 +2045,51 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
+        }
+        if ((phase & 16) || (!TAIL && (phase & 8) && __ballot(state == 6))) {
+            // hand-on records: the drain (phase 16: every busy lane's exact state, then
+            // the wave is done) or walk hand-ons (state 6: a collected hit set the
+            // certificate left undecided; the tail launch walks it exactly)
+            const bool drain = (phase & 16) != 0;
+            bool mine = drain ? state != 3 : state == 6;
+            const unsigned long long bm = __ballot(mine);
+            const int nbusy = __popcll(bm);
+            const int leader = __ffsll((long long)bm) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.cont_count + (drain ? level : kDrainLevels + level), nbusy);
+            base = __shfl(base, leader);
+            const int r = base + __popcll(bm & ((1ull << lane) - 1ull));
+            if (!drain && mine && r >= p.cont_wcap) {  // no room left: the whole ray goes to k_trace_deferred
+                p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                mine = false;
+            }
+            if (mine) {
+                int* C = cout + (drain ? r : p.cont_cap - 1 - r);
+                const size_t cs = (size_t)p.cont_cap;
+                C[kCJ * cs] = j; C[kCState * cs] = drain ? state : 5; C[kCIm * cs] = im;
+                C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
+                C[kCOw * cs] = __float_as_int(ow.x); C[(kCOw + 1) * cs] = __float_as_int(ow.y);
+                C[(kCOw + 2) * cs] = __float_as_int(ow.z);
+                C[kCDw * cs] = __float_as_int(dw.x); C[(kCDw + 1) * cs] = __float_as_int(dw.y);
+                C[(kCDw + 2) * cs] = __float_as_int(dw.z);
+                C[kCCur * cs] = cur; C[kCSp * cs] = sp;
+                C[kCLfI * cs] = lf_i; C[kCLfE * cs] = lf_e; C[kCLf2I * cs] = lf2_i; C[kCLf2E * cs] = lf2_e;
+                C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = drain ? sbase : -1;
+                C[kCX * cs] = __float_as_int(tmin); C[(kCX + 1) * cs] = nh; C[(kCX + 2) * cs] = tier;
+                C[(kCX + 3) * cs] = pblk; C[(kCX + 4) * cs] = __float_as_int(win);
+                C[(kCX + 5) * cs] = __float_as_int(t_box);
+                C[(kCX + 6) * cs] = __float_as_int(G.x); C[(kCX + 7) * cs] = __float_as_int(G.y);
+                C[(kCX + 8) * cs] = __float_as_int(G.z);
+#pragma unroll 1
+                for (int q = 0; q < (drain ? kGfStack : 0); q++) C[(kCX + 9 + q) * cs] = stack[q * BS];
+#pragma unroll 1
+                for (int q = 0; q < kGfHitCap; q++) {
+                    const int4 e = hs[q * BS];
+                    C[(kCX + 9 + kGfStack + 4 * q) * cs] = e.x; C[(kCX + 10 + kGfStack + 4 * q) * cs] = e.y;
+                    C[(kCX + 11 + kGfStack + 4 * q) * cs] = e.z; C[(kCX + 12 + kGfStack + 4 * q) * cs] = e.w;
+                }
+            }
+            state = drain ? 3 : (state == 6 ? 0 : state);
         }
         if (stamps) { const unsigned long long t = clock64(); cy[4] += t - ts; ts = t; }
     }
@@ -2292,8 +2303,9 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
         *p.defer_count = 0;        // and no deferred grid_fast rays
-        for (int l = 0; l < kDrainLevels; l++) {   // and no drain continuations
+        for (int l = 0; l < kDrainLevels; l++) {   // and no drain continuations or walk hand-ons
             p.cont_count[l] = 0;
+            p.cont_count[kDrainLevels + l] = 0;
             p.cont_next[l] = 0;
         }
     }
@@ -2637,9 +2649,13 @@ int Renderer::allocateOnGPU(const Scene& scene) {
                                                               : ((kp.trace_flags & ~1) == 10 || (kp.trace_flags & ~1) == 26);
         kp.drain_dump = split_trace && def_variant ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
+        // walk hand-ons (k_trace_gf main launch -> its level-1 tail): room for one per lane
+        const char* wh = std::getenv("PT_WALK_HANDON");
+        kp.cont_wcap = split_trace && cfg.accel == ACCEL_GRID_FAST && (gf_flags & ~1) == 8 &&
+                       (wh ? std::atoi(wh) != 0 : true) ? trace_blocks * 64 : 0;
         const char* dl = std::getenv("PT_DRAIN_LEVELS");     // tail launches; the last one runs to the end
         kp.drain_levels = std::max(1, std::min(kDrainLevels, dl ? std::atoi(dl) : 1));
-        kp.spill_stride = spills ? trace_blocks * 64 : 1;
+        kp.spill_stride = spills ? 2 * trace_blocks * 64 : 1;   // main lanes, then tail lanes' own areas
         const char* sm = std::getenv("PT_SLOTMAP");
         kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
         // Ray sort before each persistent trace (claim order only; results unchanged).
@@ -2670,6 +2686,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.drain_dump = 0;
         kp.cont_cap = 1;
     }
+    kp.cont_cap += kp.cont_wcap;
     kp.contrib = nullptr;
     pstream[0] = stream;
     for (int i = 1; i < npipes; i++) {
@@ -2730,9 +2747,9 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(hipMemsetAsync(k.trace_next, 0, sizeof(int), st));
     PT_HIP(upload(allocs, &k.iter_dev, nullptr, sizeof(int), st));
     PT_HIP(upload(allocs, &k.cont, nullptr, 2 * (size_t)k.cont_cap * kContFields * sizeof(int), st));
-    PT_HIP(upload(allocs, &k.cont_count, nullptr, kDrainLevels * sizeof(int), st));
+    PT_HIP(upload(allocs, &k.cont_count, nullptr, 2 * kDrainLevels * sizeof(int), st));
     PT_HIP(upload(allocs, &k.cont_next, nullptr, kDrainLevels * sizeof(int), st));
-    PT_HIP(hipMemsetAsync(k.cont_count, 0, kDrainLevels * sizeof(int), st));
+    PT_HIP(hipMemsetAsync(k.cont_count, 0, 2 * kDrainLevels * sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.cont_next, 0, kDrainLevels * sizeof(int), st));
     return 0;
 }
@@ -2770,7 +2787,8 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
                 else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
                 break;
         }
-        for (int l = 1; k.drain_dump > 0 && l <= k.drain_levels; l++) {   // the rays handed on, packed
+        for (int l = 1; (k.drain_dump > 0 && l <= k.drain_levels) || (k.cont_wcap > 0 && l == 1); l++) {
+            // the rays handed on (drain continuations; walk hand-ons go to level 1), packed
             if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b, l);
             else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b, l);
         }
