@@ -2015,7 +2015,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (PT_TRACE_STATS && (p.debug & 128) && pblk < 0) {      // timing-only ablation: no walk at all
                 w.hit = true; w.has_best = true; w.final_min = true; w.t = tmin; w.tri = -1; w.tw = 0.0f;
                 for (int h = 0; h < nh; h++) if (__int_as_float(hs[h * BS].x) == tmin) w.tri = hs[h * BS].y;
-            } else if (!TAIL && PT_WALK_DEFER) {
+            } else if (!TAIL && !(F & 16) && PT_WALK_DEFER) {
                 // the certificate only; a ray it cannot decide is handed on to the tail launch
                 // (which walks it exactly) or, past the records' room, to k_trace_deferred
                 int tri = -1;
@@ -2650,9 +2650,15 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.drain_dump = split_trace && def_variant ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
         // walk hand-ons (k_trace_gf main launch -> its level-1 tail): room for one per lane
+        // (PT_WALK_WCAP overrides; beyond it a ray goes whole to k_trace_deferred).  With one
+        // pipeline the serial tail costs more than the in-place walk saves (measured 927 vs
+        // 1306 Mrays/s at configs[1]; 16 pipelines: +2 %), so the main launch walks in place
+        // there (variant F | 16) unless PT_WALK_HANDON=1 asks for hand-ons.
         const char* wh = std::getenv("PT_WALK_HANDON");
-        kp.cont_wcap = split_trace && cfg.accel == ACCEL_GRID_FAST && (gf_flags & ~1) == 8 &&
-                       (wh ? std::atoi(wh) != 0 : true) ? trace_blocks * 64 : 0;
+        const char* wc = std::getenv("PT_WALK_WCAP");
+        const bool handon = wh ? std::atoi(wh) != 0 : npipes > 1;
+        kp.cont_wcap = split_trace && cfg.accel == ACCEL_GRID_FAST && (gf_flags & ~1) == 8 && handon
+                           ? (wc ? std::max(0, std::atoi(wc)) : trace_blocks * 64) : 0;
         const char* dl = std::getenv("PT_DRAIN_LEVELS");     // tail launches; the last one runs to the end
         kp.drain_levels = std::max(1, std::min(kDrainLevels, dl ? std::atoi(dl) : 1));
         kp.spill_stride = spills ? 2 * trace_blocks * 64 : 1;   // main lanes, then tail lanes' own areas
@@ -2782,9 +2788,14 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0); break;
             case 12: hipLaunchKernelGGL((k_trace_gf<64, 12>), g, t, 0, st, k, b, 0); break;
             case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b, 0); break;
-            default:                         // 9; 8 when the model records do not fit LDS
-                if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
-                else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
+            default:                         // 9; 8 when the model records do not fit LDS; | 16: walks in place
+                if (k.cont_wcap > 0) {
+                    if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
+                    else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
+                } else {
+                    if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 25>), g, t, 0, st, k, b, 0);
+                    else hipLaunchKernelGGL((k_trace_gf<64, 24>), g, t, 0, st, k, b, 0);
+                }
                 break;
         }
         for (int l = 1; (k.drain_dump > 0 && l <= k.drain_levels) || (k.cont_wcap > 0 && l == 1); l++) {

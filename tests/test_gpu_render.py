@@ -477,22 +477,25 @@ def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, mo
     assert_bitexact(img, oimg, f"PT_DRAIN_DUMP={dump} PT_DRAIN_LEVELS={levels} {scene}")
 
 
-@pytest.mark.parametrize("handon,pipes", [(1, 1), (1, 4), (0, 1), (0, 4)])
+@pytest.mark.parametrize("handon,wcap,pipes", [(1, None, 1), (1, None, 4), (0, None, 1), (0, None, 4), (1, 7, 4)])
 @pytest.mark.parametrize("scene", ["synthetic", "reference"])
-def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, handon, pipes, scene):
-    """k_trace_gf's main launch runs only the walk certificate; a hit set it
-    cannot decide is handed on (PT_WALK_HANDON=1, default) to the level-1 tail
-    launch, which walks it exactly and continues the ray, or (PT_WALK_HANDON=0,
-    or no record room left) the whole ray goes to k_trace_deferred.  Both
-    routes, with and without drain continuations (pipes 1 / 4), keep the
-    oracle's images and segment counts."""
+def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, handon, wcap, pipes, scene):
+    """k_trace_gf's main launch runs only the walk certificate when walk
+    hand-ons are on (PT_WALK_HANDON=1; default with several pipelines): a hit
+    set it cannot decide is handed on to the level-1 tail launch, which walks
+    it exactly and continues the ray; past the records' room (PT_WALK_WCAP=7
+    here) the whole ray goes to k_trace_deferred.  PT_WALK_HANDON=0 (default
+    with one pipeline) walks in place.  Every route, with and without drain
+    continuations (pipes 1 / 4), keeps the oracle's images and segment counts."""
     from pathtracerap_amd import synthetic
     P, O = pt_mod, oracle_mod
     monkeypatch.setenv("PT_WALK_HANDON", str(handon))
+    if wcap is not None:
+        monkeypatch.setenv("PT_WALK_WCAP", str(wcap))
     path = synthetic.diffuse_scene(synth_dir, ntri=6000, seed=29, metallic=True) if scene == "synthetic" else REF_SCENE
     s = P.Scene(path)
     s.build(bvh=True)
     cfg = P.RenderConfig(width=173, height=89, iterations=3, max_bounces=7, accel=P.ACCEL_GRID_FAST, pipelines=pipes)
     img, seg, oimg, oseg = _render_both(P, O, s, cfg)
     assert seg == oseg
-    assert_bitexact(img, oimg, f"PT_WALK_HANDON={handon} pipes={pipes} {scene}")
+    assert_bitexact(img, oimg, f"PT_WALK_HANDON={handon} PT_WALK_WCAP={wcap} pipes={pipes} {scene}")
