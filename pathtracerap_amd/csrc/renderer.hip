@@ -238,8 +238,8 @@ __device__ __forceinline__ bool bvh_step(const KParams& p, f3 o, f3 d, f3 inv, i
     float tn0, tf0, tn1, tf1;
     node_slab(lo0, hi0, o, inv, tn0, tf0);
     node_slab(lo1, hi1, o, inv, tn1, tf1);
-    bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
-    bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
+    bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= best);
+    bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= best);
 #pragma unroll
     for (int c = 0; c < 2; c++) {
         const bool hc = c == 0 ? h0 : h1;
@@ -329,8 +329,8 @@ __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 i
         node_slab(lo0, hi0, o, inv, tn0, tf0);
         node_slab(lo1, hi1, o, inv, tn1, tf1);
         const float bound = BOUNDED ? tmin + margin : 3.0e38f;
-        bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= bound;
-        bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= bound;
+        bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= bound);
+        bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= bound);
 #pragma unroll
         for (int c = 0; c < 2; c++) {
             const bool hc = c == 0 ? h0 : h1;
@@ -1106,7 +1106,15 @@ __device__ __forceinline__ void spush_t(int* stack, int* spill, int stride, int 
 }
 template <int BS, int SCAP = kStack>
 __device__ __forceinline__ int spop_t(const int* stack, const int* spill, int stride, int sp) {
-    return sp < SCAP ? stack[sp * BS] : spill[(size_t)(sp - SCAP) * stride];
+    // Written as a select of the two addresses, the compiler merged the loads
+    // into one flat load (which waits on both the LDS and the vector memory
+    // counters) on every pop.  Typed LDS / global pointers keep them apart: the
+    // LDS read is unconditional (clamped index), the spill read has its own branch.
+    typedef __attribute__((address_space(3))) const int lds_int;
+    typedef __attribute__((address_space(1))) const int glb_int;
+    int v = ((lds_int*)stack)[min(sp, SCAP - 1) * BS];
+    if (sp >= SCAP) v = ((glb_int*)spill)[(size_t)(sp - SCAP) * stride];
+    return v;
 }
 #define spush(stack, spill, sp, e) spush_t<BS>(stack, spill, p.spill_stride, sp, e)
 #define spop(stack, spill, sp) spop_t<BS>(stack, spill, p.spill_stride, sp)
@@ -1244,7 +1252,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 const int leader = __ffsll((long long)idle) - 1;
                 int base = 0;
                 if (lane == leader) base = atomicAdd(p.cont_next + level - 1, cnt);
-                base = __shfl(base, leader);
+                base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
                 if (base + cnt >= ncont) exhausted = true;
                 if (state == 0) {
                     const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
@@ -1283,7 +1291,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     if (q_pos >= q_cnt) {                           // claim the next non-empty source block
                         int b = 0;
                         if (lane == 0) b = atomicAdd(p.trace_next, 1);
-                        b = __shfl(b, 0);
+                        b = __builtin_amdgcn_readlane(b, 0);
                         if (b >= nb) { exhausted = true; break; }
                         q_b = b; q_pos = 0; q_cnt = p.blk_cnt[b]; q_off = p.blk_off[b];
                         continue;
@@ -1310,7 +1318,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 const int leader = __ffsll((long long)idle) - 1;
                 int base = 0;
                 if (lane == leader) base = atomicAdd(p.trace_next, cnt);
-                base = __shfl(base, leader);
+                base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
                 if (base + cnt >= n) exhausted = true;
                 if (state == 0) {
                     j = base + __popcll(idle & ((1ull << lane) - 1ull));
@@ -1350,6 +1358,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
+        phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
             {
@@ -1368,7 +1377,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             const int leader = __ffsll((long long)bm) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.cont_count + level, nbusy);
-            base = __shfl(base, leader);
+            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             if (state != 3) {
                 int* C = cout + base + __popcll(bm & ((1ull << lane) - 1ull));
                 const size_t cs = (size_t)p.cont_cap;
@@ -1503,8 +1512,8 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 float tn0, tf0, tn1, tf1;
                 node_slab(lo0, hi0, o, ninv, tn0, tf0);
                 node_slab(lo1, hi1, o, ninv, tn1, tf1);
-                const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tn0 <= best;
-                const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tn1 <= best;
+                const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= best);
+                const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= best);
                 const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
                 const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
                 // next node after the leaves: same rule as bvh_step
@@ -1701,7 +1710,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.cont_next + level - 1, cnt);
-            base = __shfl(base, leader);
+            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             if (base + cnt >= ncont) exhausted = true;
             if (state == 0) {
                 const int r = base + __popcll(idle & ((1ull << lane) - 1ull));
@@ -1750,7 +1759,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 if (q_pos >= q_cnt) {
                     int b = 0;
                     if (lane == 0) b = atomicAdd(p.trace_next, 1);
-                    b = __shfl(b, 0);
+                    b = __builtin_amdgcn_readlane(b, 0);
                     if (b >= nb_prev) { exhausted = true; break; }
                     q_b = b; q_pos = 0; q_cnt = p.blk_cnt[b]; q_off = p.blk_off[b];
                     continue;
@@ -1775,7 +1784,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.trace_next, cnt);
-            base = __shfl(base, leader);
+            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             if (base + cnt >= n) exhausted = true;
             if (state == 0) {
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
@@ -1811,6 +1820,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
+        phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
             {
@@ -1960,8 +1970,11 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
             const float X = tmin + win;
             const float bound = X + gf_slack(X, t_box);
-            const bool h0 = cnt0 >= 0 && tn0 <= tf0 && tf0 >= -kEps && tx0 <= bound;
-            const bool h1 = cnt1 >= 0 && tn1 <= tf1 && tf1 >= -kEps && tx1 <= bound;
+            // non-short-circuit: both children's slabs in one basic block (a branch on
+            // cnt >= 0 moved the float work into its own block, where every min/max
+            // operand was re-canonicalised)
+            const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
+            const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
             const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
             const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
             int next = -1;
@@ -2057,7 +2070,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int leader = __ffsll((long long)bm) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.cont_count + (drain ? level : kDrainLevels + level), nbusy);
-            base = __shfl(base, leader);
+            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             const int r = base + __popcll(bm & ((1ull << lane) - 1ull));
             if (!drain && mine && r >= p.cont_wcap) {  // no room left: the whole ray goes to k_trace_deferred
                 p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
