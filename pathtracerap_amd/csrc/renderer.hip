@@ -1885,73 +1885,80 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const float4 A0 = p.bvh_tri_geom[3 * lf_i], B0 = p.bvh_tri_geom[3 * lf_i + 1], C0 = p.bvh_tri_geom[3 * lf_i + 2];
             const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
             const int n_step = i1 != lf_i ? 2 : 1;
+            // Both tests first (pure), then the hits' insertions in leaf order: the loop
+            // below runs only for lanes with a hit, and carries 4 values instead of 12.
+            float t0 = 0.0f, t1 = 0.0f;
+            const bool hit0 = tri_test_rec(A0, B0, C0, o, d, t0);
+            const bool hit1 = tri_test_rec(A1, B1, C1, o, d, t1) & (n_step == 2);
+            if (hit0 | hit1) {
 #pragma unroll 1
-            for (int k = 0; k < n_step && state == 4; k++) {
-                const float4 A = k ? A1 : A0, B = k ? B1 : B0, C = k ? C1 : C0;
-                float t;
-                if (tri_test_rec(A, B, C, o, d, t)) {
-                    if (t < tmin) tmin = t;
-                    const ModelRec& M = models[im];
-                    const float X = tmin + win;
-                    const float Xs = X + gf_slack(X, t_box);
-                    if (!(vbox_entry(M, __float_as_int(B.w), __float_as_int(C.w), o, ninv) > Xs)) {   // required member
-                        const int4 e = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
-                                                 __float_as_int(C.w));
-                        if (pblk < 0) {
-                            if (nh == kGfHitCap) {          // drop members now beyond the bound
-                                int wn = 0;
-                                for (int q = 0; q < nh; q++) {
-                                    const int4 x = hs[q * BS];
-                                    if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) hs[(wn++) * BS] = x;
+                for (int k = 0; k < n_step && state == 4; k++) {
+                    const float t = k ? t1 : t0;
+                    const int aw = __float_as_int(k ? A1.w : A0.w), bw = __float_as_int(k ? B1.w : B0.w),
+                              cw = __float_as_int(k ? C1.w : C0.w);
+                    if (k ? hit1 : hit0) {
+                        if (t < tmin) tmin = t;
+                        const ModelRec& M = models[im];
+                        const float X = tmin + win;
+                        const float Xs = X + gf_slack(X, t_box);
+                        if (!(vbox_entry(M, bw, cw, o, ninv) > Xs)) {   // required member
+                            const int4 e = make_int4(__float_as_int(t), aw, bw, cw);
+                            if (pblk < 0) {
+                                if (nh == kGfHitCap) {          // drop members now beyond the bound
+                                    int wn = 0;
+                                    for (int q = 0; q < nh; q++) {
+                                        const int4 x = hs[q * BS];
+                                        if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) hs[(wn++) * BS] = x;
+                                    }
+                                    nh = wn;
                                 }
-                                nh = wn;
-                            }
-                            if (nh == kGfHitCap) {          // LDS full: continue in a 64-member global pool block
-                                const int blk = atomicAdd(p.hs_pool_next, 1);
-                                if (blk < p.hs_pool_blocks) {
-                                    pblk = blk;
-                                    int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
-                                    for (int q = 0; q < nh; q++) g[q] = hs[q * BS];
+                                if (nh == kGfHitCap) {          // LDS full: continue in a 64-member global pool block
+                                    const int blk = atomicAdd(p.hs_pool_next, 1);
+                                    if (blk < p.hs_pool_blocks) {
+                                        pblk = blk;
+                                        int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
+                                        for (int q = 0; q < nh; q++) g[q] = hs[q * BS];
+                                    }
                                 }
                             }
-                        }
-                        if (pblk >= 0) {
-                            int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
-                            if (nh == kHitCapPool) {
-                                int wn = 0;
-                                for (int q = 0; q < nh; q++) {
-                                    const int4 x = g[q];
-                                    if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) g[wn++] = x;
+                            if (pblk >= 0) {
+                                int4* g = p.hs_pool + (size_t)pblk * kHitCapPool;
+                                if (nh == kHitCapPool) {
+                                    int wn = 0;
+                                    for (int q = 0; q < nh; q++) {
+                                        const int4 x = g[q];
+                                        if (!(vbox_entry(M, x.z, x.w, o, ninv) > Xs)) g[wn++] = x;
+                                    }
+                                    nh = wn;
                                 }
-                                nh = wn;
+                                if (nh < kHitCapPool) g[nh++] = e;
+                                else { p.defer_slots[atomicAdd(p.defer_count, 1)] = j; state = 0; }   // pool block full too
+                            } else if (nh < kGfHitCap) {
+                                hs[nh * BS] = e;
+                                nh++;
+                            } else {                            // pool exhausted: the whole ray goes to k_trace_deferred
+                                p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
+                                state = 0;
                             }
-                            if (nh < kHitCapPool) g[nh++] = e;
-                            else { p.defer_slots[atomicAdd(p.defer_count, 1)] = j; state = 0; }   // pool block full too
-                        } else if (nh < kGfHitCap) {
-                            hs[nh * BS] = e;
-                            nh++;
-                        } else {                            // pool exhausted: the whole ray goes to k_trace_deferred
-                            p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
-                            state = 0;
                         }
                     }
                 }
-                if (state == 4) {
-                    lf_i++;
-                    if (lf_i == lf_e) {
-                        if (lf2_i < lf2_e) {
-                            lf_i = lf2_i; lf_e = lf2_e;
-                            lf2_i = lf2_e = 0;
-                        } else if (lf_next >= 0) {
-                            cur = lf_next;
-                            state = 2;
-                        } else if (sp == 0) {
-                            collected = true;
-                        } else {
-                            sp--;
-                            cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
-                            state = 2;
-                        }
+            }
+            if (state == 4) {
+                lf_i += n_step;                     // with two, the first never ends the list
+                if (lf_i == lf_e) {
+                    if (lf2_i < lf2_e) {
+                        lf_i = lf2_i; lf_e = lf2_e;
+                        lf2_i = lf2_e = 0;
+                    } else if (lf_next >= 0) {
+                        cur = lf_next;
+                        state = 2;
+                    } else if (sp == 0) {
+                        collected = true;
+                    } else {
+                        sp--;
+                        cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
+                        state = 2;
                     }
                 }
             }
