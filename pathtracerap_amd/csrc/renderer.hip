@@ -935,9 +935,12 @@ template <int ACCEL>
 __device__ __forceinline__ bool model_culled(const ModelRec& M, f3 orig, f3 dir, f3 winv, float dlen, float gdist) {
     float wtn, wtf;
     node_slab(M.wbox, M.wbox + 3, orig, winv, wtn, wtf);
-    if (wtn * dlen > gdist * 1.0001f + 0.01f) return true;           // cannot beat the current hit
-    if (wtn > wtf || wtf * dlen < -1.0f) {                            // misses the instance box
-        if (ACCEL == ACCEL_BVH) return true;
+    // both tests in one block (`|`, not `||`: a branch between them re-canonicalised the slab operands)
+    const bool beyond = wtn * dlen > gdist * 1.0001f + 0.01f;        // cannot beat the current hit
+    const bool miss = (wtn > wtf) | (wtf * dlen < -1.0f);             // misses the instance box
+    if (ACCEL == ACCEL_BVH) return beyond | miss;
+    if (beyond | miss) {
+        if (beyond) return true;
         const f3 dm = xform12(M.w2m, dir, 0.0f);
         if (dm.x != 0.0f && dm.y != 0.0f && dm.z != 0.0f) return true;
     }
