@@ -177,6 +177,11 @@ def main():
     # warmup: builds the primary-hit cache, warms caches/clocks; distinct iteration ids
     r.renderLoop(first_iter=1_000_000 + rank * max(W, 1), n_iters=W, sync=False)
     torch.cuda.synchronize(dev)
+    if world > 1:
+        # warm the accumulator-sized all-reduce too: any one-time RCCL setup for a
+        # message of this size is paid here, not inside the timed region
+        dist.all_reduce(image, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize(dev)
     r.clearImage()
     seg0 = r.segments()
     pb0 = r.segments_per_bounce()
