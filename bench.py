@@ -131,6 +131,20 @@ def load_pmc(kernel, workload_key):
         return None
 
 
+VALU_PEAK_G = 256 * 4 * 2.4 / 2   # G wave-instructions/s: 1024 SIMDs, one wave64 VALU op per 2 cycles at 2.4 GHz
+
+
+def load_sq(workload_key, tag="_sq"):
+    """VALU / SALU wave-instruction counts of the committed rocprofv3
+    SQ_INSTS_VALU / SQ_INSTS_SALU pass (scripts/pmc_summary.py sq): tag "_sq" with
+    the bench's pipelines, "_sq_p1" with one pipeline; None when absent."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as f:
+            return json.load(f).get(workload_key, {}).get(tag)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     if args.hw_queues > 0:     # read once by the HIP runtime at initialisation: set before torch touches it
@@ -317,6 +331,28 @@ def main():
                     "shading_pass": shade,
                     "first_bounce_avg_ms": round(stats["first_ms"] / max(stats["first_launches"], 1), 4),
                     "scan_avg_ms": round(stats["scan_ms"] / max(stats["scan_launches"], 1), 4)}
+        # Issue roofline: the traces are bound by instruction issue and dependent-load
+        # latency, not by HBM bytes, so the VALU issue rate against the SIMDs' peak is
+        # the informative fraction -- for the whole job (all kernels of a step, with the
+        # pipelines overlapping) and for the dominant kernel's single-pipeline launches.
+        issue = None
+        sq = load_sq(workload_key)
+        if sq:
+            v_step = sq["valu_insts_per_iteration"]
+            job = v_step * K / elapsed / 1e9          # per GPU: each rank runs K steps in `elapsed`
+            issue = {"bound": "valu", "unit": "G wave-instr/s", "peak": VALU_PEAK_G,
+                     "job": {"valu_insts_per_step": round(v_step), "achieved": round(job, 1),
+                             "frac": round(job / VALU_PEAK_G, 4),
+                             "salu_insts_per_step": round(sq["salu_insts_per_iteration"]),
+                             "salu_achieved": round(sq["salu_insts_per_iteration"] * K / elapsed / 1e9, 1)},
+                     "source": "rocprofv3 SQ_INSTS_VALU / SQ_INSTS_SALU pass (profiles/pmc_latest.json)"}
+            sq1 = load_sq(workload_key, "_sq_p1")     # the roofline pass runs one pipeline
+            kk = sq1["kernels"].get(roof["kernel"]) if (roof and sq1) else None
+            if kk:
+                ach = kk["valu_insts_per_launch"] / (roof["avg_launch_ms"] / 1e3) / 1e9
+                issue["kernel"] = {"name": roof["kernel"], "valu_insts_per_launch": round(kk["valu_insts_per_launch"]),
+                                   "avg_launch_ms": roof["avg_launch_ms"], "achieved": round(ach, 1),
+                                   "frac": round(ach / VALU_PEAK_G, 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -336,7 +372,7 @@ def main():
                        "parallelism": f"samples sharded x{world}" + (" (gloo rehearsal)" if world > 1 and args.dist_backend == "gloo" else ""), "pipelines": pipes,
                        "segments": int(seg_total), "segments_per_bounce_rank0": per_bounce,
                        "image_finite": img_ok, "trace_faults": faults},
-            "roofline": roof, "cpu_baseline": cpu, "alt_mode": alt,
+            "roofline": roof, "issue_roofline": issue, "cpu_baseline": cpu, "alt_mode": alt,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

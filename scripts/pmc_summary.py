@@ -3,6 +3,9 @@
 profiles/pmc_latest.json (read by bench.py for roofline.traffic).
 
     python scripts/pmc_summary.py WORKLOAD_KEY FETCH_DIR WRITE_DIR [OUT_JSON]
+    python scripts/pmc_summary.py sq WORKLOAD_KEY SQ_DIR ITERATIONS [TAG [OUT_JSON]]
+      (TAG "_sq": the bench's pipelines, for the whole-job issue rate; "_sq_p1": one
+      pipeline, matching bench.py's per-kernel roofline pass)
 
 Per MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so
@@ -30,6 +33,11 @@ KERNELS = {
     "k_trace_gf<": "k_trace_gf",
     "k_trace_deferred": "k_trace_deferred",
     "k_bounce<false, 3,": "k_bounce<false,hitbuf>",
+    "k_sort_hist": "k_sort_hist",
+    "k_sort_prefix": "k_sort_prefix",
+    "k_sort_scatter": "k_sort_scatter",
+    "k_merge": "k_merge",
+    "k_primary": "k_primary",
 }
 
 
@@ -46,6 +54,34 @@ def read_counter(d, counter):
                     if k in name:
                         per[short].append(float(row["Counter_Value"]))
     return per
+
+
+def main_sq(key, sq_dir, iterations, tag="_sq", out=None):
+    """SQ_INSTS_VALU / SQ_INSTS_SALU pass (wave-level instruction counts, chip
+    totals per dispatch): per-kernel counts per launch, and the total of the
+    renderer's kernels over the `iterations` iterations the profiled command ran
+    (bench.py: warmup + steps).  bench.py turns these into an issue roofline."""
+    out = out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
+    valu = read_counter(sq_dir, "SQ_INSTS_VALU")
+    salu = read_counter(sq_dir, "SQ_INSTS_SALU")
+    per = {}
+    tot_v = tot_s = 0.0
+    for k in set(valu) | set(salu):
+        v, sa = valu.get(k, []), salu.get(k, [])
+        per[k] = {"valu_insts_per_launch": sum(v) / max(len(v), 1), "salu_insts_per_launch": sum(sa) / max(len(sa), 1),
+                  "launches": max(len(v), len(sa))}
+        if k != "k_primary":
+            tot_v += sum(v)
+            tot_s += sum(sa)
+    data = {}
+    if os.path.exists(out):
+        with open(out) as fh:
+            data = json.load(fh)
+    data.setdefault(key, {})[tag] = {"iterations": int(iterations), "valu_insts_per_iteration": tot_v / int(iterations),
+                                       "salu_insts_per_iteration": tot_s / int(iterations), "kernels": per}
+    with open(out, "w") as fh:
+        json.dump(data, fh, indent=1, sort_keys=True)
+    print(json.dumps(data[key][tag], indent=1))
 
 
 def main(key, fetch_dir, write_dir, out=None):
@@ -66,11 +102,14 @@ def main(key, fetch_dir, write_dir, out=None):
     if os.path.exists(out):
         with open(out) as fh:
             data = json.load(fh)
-    data[key] = res
+    data.setdefault(key, {}).update(res)
     with open(out, "w") as fh:
         json.dump(data, fh, indent=1, sort_keys=True)
     print(json.dumps({key: res}, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    if sys.argv[1] == "sq":
+        main_sq(*sys.argv[2:])
+    else:
+        main(*sys.argv[1:])
