@@ -107,31 +107,35 @@ __device__ __forceinline__ bool slab_ref(const float* bb, f3 o, f3 d, f3 inv, fl
 // ~1e-7 relative against a 4e-5 margin), so the exact float sequence below
 // decides every remaining case exactly as the reference does.
 __device__ __forceinline__ bool tri_test_rec(const float4 A, const float4 B, const float4 C, f3 o, f3 d, float& t_out) {
+    // Conditions combined with `&` (same comparisons, same NaN behaviour as the
+    // early returns): one branch into the exact test instead of one per
+    // condition -- the traces are issue-bound, and every divergent early return
+    // cost a handful of scalar exec-mask instructions.
     const f3 v0 = mk3(A.x, A.y, A.z), e1 = mk3(B.x, B.y, B.z), e2 = mk3(C.x, C.y, C.z);
     f3 pvec = cross(d, e2);
     float det = dot(e1, pvec);
-    if (absr(det - 0.0f) < kEps) return false;
     f3 tvec = o - v0;
     const float a = dot(tvec, pvec);
     const float sg = det > 0.0f ? 1.0f : -1.0f;
     const float D = det * sg;
     const float as = a * sg;
-    if (as < -0.0052f * D || as > 1.0052f * D) return false;           // u certainly out
     f3 qvec = cross(tvec, e1);
     const float b = dot(d, qvec);
     const float bs = b * sg;
-    if (bs < -0.0052f * D || (as + bs) > 1.0052f * D) return false;   // v or u+v certainly out
     const float c = dot(e2, qvec);
-    if (c * sg < -0.0052f * D) return false;                            // t certainly < -eps
+    const bool screen = !(absr(det - 0.0f) < kEps) &
+                        !(as < -0.0052f * D) & !(as > 1.0052f * D) &            // u certainly out
+                        !(bs < -0.0052f * D) & !((as + bs) > 1.0052f * D) &     // v or u+v certainly out
+                        !(c * sg < -0.0052f * D);                               // t certainly < -eps
+    if (!screen) return false;
     float inv_det = 1 / det;
     float u = a * inv_det;
-    if (u < 0.0f - kEps || u > 1.0f + kEps) return false;
     float v = b * inv_det;
-    if (v < 0.0f - kEps || u + v > 1.0f + kEps) return false;
     float t = c * inv_det;
-    if (t < 0.0f - kEps) return false;
-    t_out = t;
-    return true;
+    const bool hit = !(u < 0.0f - kEps) & !(u > 1.0f + kEps) & !(v < 0.0f - kEps) & !(u + v > 1.0f + kEps) &
+                     !(t < 0.0f - kEps);
+    if (hit) t_out = t;
+    return hit;
 }
 
 __device__ __forceinline__ bool tri_test(const float4* __restrict__ tg, int it, f3 o, f3 d, float& t_out) {
