@@ -1123,6 +1123,16 @@ __device__ __forceinline__ int spop_t(const int* stack, const int* spill, int st
     if (sp >= SCAP) v = ((glb_int*)spill)[(size_t)(sp - SCAP) * stride];
     return v;
 }
+// Pop for the lanes with `take`, without a branch around the LDS read: every lane
+// reads its (clamped) LDS entry; only a spilled entry is read under a branch.
+template <int BS, int SCAP = kStack>
+__device__ __forceinline__ int spop_if(bool take, const int* stack, const int* spill, int stride, int sp) {
+    typedef __attribute__((address_space(3))) const int lds_int;
+    typedef __attribute__((address_space(1))) const int glb_int;
+    int v = ((lds_int*)stack)[min(max(sp, 0), SCAP - 1) * BS];
+    if (take & (sp >= SCAP)) v = ((glb_int*)spill)[(size_t)(sp - SCAP) * stride];
+    return v;
+}
 #define spush(stack, spill, sp, e) spush_t<BS>(stack, spill, p.spill_stride, sp, e)
 #define spop(stack, spill, sp) spop_t<BS>(stack, spill, p.spill_stride, sp)
 
@@ -1465,20 +1475,21 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     if (e & 1) { lf_i = e >> 4; lf_e = lf_i + ((e >> 1) & 7); }
                     else { cur = e >> 1; state = 2; }
                 }
-            } else if (lf_i == lf_e) {
-                if (lf2_i < lf2_e) {                    // second leaf child
-                    lf_i = lf2_i; lf_e = lf2_e;
-                    lf2_i = lf2_e = 0;
-                } else if (lf_next >= 0) {
-                    cur = lf_next;
-                    state = 2;
-                } else if (sp == 0) {
-                    model_done = true;
-                } else {
-                    sp--;
-                    cur = stack[sp * BS];
-                    state = 2;
-                }
+            } else if (!(F & 16)) {
+                // end of the leaf: second leaf child, `next`, or the stack (selects)
+                const bool end = lf_i == lf_e;
+                const bool second = end & (lf2_i < lf2_e);
+                const bool tonext = end & !second & (lf_next >= 0);
+                const bool pop = end & !second & !tonext & (sp > 0);
+                model_done = end & !second & !tonext & (sp == 0);
+                const int top = stack[max(sp - 1, 0) * BS];
+                lf_i = second ? lf2_i : lf_i;
+                lf_e = second ? lf2_e : lf_e;
+                lf2_i = second ? 0 : lf2_i;
+                lf2_e = second ? 0 : lf2_e;
+                cur = tonext ? lf_next : (pop ? top : cur);
+                state = (tonext | pop) ? 2 : state;
+                sp -= pop ? 1 : 0;
             }
         } else if ((phase & 2) && state == 2) {
             if (F & 16) {
@@ -1521,39 +1532,27 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 node_slab(lo1, hi1, o, ninv, tn1, tf1);
                 const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= best);
                 const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= best);
-                const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
-                const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
-                // next node after the leaves: same rule as bvh_step
-                int next = -1;
-                if (i0 && i1) {
-                    const bool first0 = tn0 <= tn1;
-                    stack[sp * BS] = first0 ? link1 : link0;
-                    sp++;
-                    next = first0 ? link0 : link1;
-                } else if (i0) {
-                    next = link0;
-                } else if (i1) {
-                    next = link1;
-                }
-                if (l0 && l1) {                 // leaf 0, then leaf 1, then `next`
-                    lf_i = link0; lf_e = link0 + cnt0;
-                    lf2_i = link1; lf2_e = link1 + cnt1;
-                    lf_next = next;
-                    state = 4;
-                } else if (l0 || l1) {
-                    lf_i = l0 ? link0 : link1;
-                    lf_e = lf_i + (l0 ? cnt0 : cnt1);
-                    lf2_i = lf2_e = 0;
-                    lf_next = next;
-                    state = 4;
-                } else if (next >= 0) {
-                    cur = next;
-                } else if (sp == 0) {
-                    model_done = true;
-                } else {
-                    sp--;
-                    cur = stack[sp * BS];
-                }
+                // next node after the leaves: same rule as bvh_step; the decisions as
+                // selects, only the push and the (LDS) stack-top read touch memory
+                const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
+                const bool i0 = h0 & (cnt0 == 0), i1 = h1 & (cnt1 == 0);
+                const bool both = i0 & i1;
+                const bool first0 = tn0 <= tn1;
+                const int next = both ? (first0 ? link0 : link1) : (i0 ? link0 : (i1 ? link1 : -1));
+                if (both) stack[sp * BS] = first0 ? link1 : link0;
+                sp += both ? 1 : 0;
+                const bool leaf = l0 | l1;              // leaf 0, then leaf 1, then `next`
+                const bool pop = !leaf & (next < 0) & (sp > 0);
+                const int top = stack[max(sp - 1, 0) * BS];
+                model_done = !leaf & (next < 0) & (sp == 0);
+                sp -= pop ? 1 : 0;
+                cur = leaf ? cur : (next >= 0 ? next : (pop ? top : cur));
+                lf_i = leaf ? (l0 ? link0 : link1) : lf_i;
+                lf_e = leaf ? lf_i + (l0 ? cnt0 : cnt1) : lf_e;
+                lf2_i = leaf ? ((l0 & l1) ? link1 : 0) : lf2_i;
+                lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
+                lf_next = leaf ? next : lf_next;
+                state = leaf ? 4 : state;
             }
         }
         if (model_done) {
@@ -1953,21 +1952,20 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             }
             if (state == 4) {
                 lf_i += n_step;                     // with two, the first never ends the list
-                if (lf_i == lf_e) {
-                    if (lf2_i < lf2_e) {
-                        lf_i = lf2_i; lf_e = lf2_e;
-                        lf2_i = lf2_e = 0;
-                    } else if (lf_next >= 0) {
-                        cur = lf_next;
-                        state = 2;
-                    } else if (sp == 0) {
-                        collected = true;
-                    } else {
-                        sp--;
-                        cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
-                        state = 2;
-                    }
-                }
+                // end of the leaf: second leaf child, `next`, or the stack (selects)
+                const bool end = lf_i == lf_e;
+                const bool second = end & (lf2_i < lf2_e);
+                const bool tonext = end & !second & (lf_next >= 0);
+                const bool pop = end & !second & !tonext & (sp > 0);
+                collected = end & !second & !tonext & (sp == 0);
+                const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
+                lf_i = second ? lf2_i : lf_i;
+                lf_e = second ? lf2_e : lf_e;
+                lf2_i = second ? 0 : lf2_i;
+                lf2_e = second ? 0 : lf2_e;
+                cur = tonext ? lf_next : (pop ? top : cur);
+                state = (tonext | pop) ? 2 : state;
+                sp -= pop ? 1 : 0;
             }
         } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
             const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
@@ -1989,34 +1987,27 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             // operand was re-canonicalised)
             const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
             const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
-            const bool l0 = h0 && cnt0 > 0, l1 = h1 && cnt1 > 0;
-            const bool i0 = h0 && cnt0 == 0, i1 = h1 && cnt1 == 0;
-            int next = -1;
-            if (i0 && i1) {
-                const bool first0 = tn0 <= tn1;         // near child first tightens the bound
-                spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, first0 ? link1 : link0);
-                sp++;
-                next = first0 ? link0 : link1;
-            } else if (i0) {
-                next = link0;
-            } else if (i1) {
-                next = link1;
-            }
-            if (l0 || l1) {                             // leaf 0, then leaf 1, then `next`
-                lf_i = l0 ? link0 : link1;
-                lf_e = lf_i + (l0 ? cnt0 : cnt1);
-                lf2_i = (l0 && l1) ? link1 : 0;
-                lf2_e = (l0 && l1) ? link1 + cnt1 : 0;
-                lf_next = next;
-                state = 4;
-            } else if (next >= 0) {
-                cur = next;
-            } else if (sp == 0) {
-                collected = true;
-            } else {
-                sp--;
-                cur = spop_t<BS, kGfStack>(stack, spill, p.spill_stride, sp);
-            }
+            // the step's decisions as selects; only the push and the pop touch memory
+            // (the traces are issue-bound: every divergent branch costs scalar exec-mask work)
+            const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
+            const bool i0 = h0 & (cnt0 == 0), i1 = h1 & (cnt1 == 0);
+            const bool both = i0 & i1;
+            const bool first0 = tn0 <= tn1;             // near child first tightens the bound
+            const int next = both ? (first0 ? link0 : link1) : (i0 ? link0 : (i1 ? link1 : -1));
+            if (both) spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, first0 ? link1 : link0);
+            sp += both ? 1 : 0;
+            const bool leaf = l0 | l1;                  // leaf 0, then leaf 1, then `next`
+            const bool pop = !leaf & (next < 0) & (sp > 0);
+            const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
+            collected = !leaf & (next < 0) & (sp == 0);
+            sp -= pop ? 1 : 0;
+            cur = leaf ? cur : (next >= 0 ? next : (pop ? top : cur));
+            lf_i = leaf ? (l0 ? link0 : link1) : lf_i;
+            lf_e = leaf ? lf_i + (l0 ? cnt0 : cnt1) : lf_e;
+            lf2_i = leaf ? ((l0 & l1) ? link1 : 0) : lf2_i;
+            lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
+            lf_next = leaf ? next : lf_next;
+            state = leaf ? 4 : state;
         }
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
         if (collected) {
