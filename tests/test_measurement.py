@@ -1,0 +1,64 @@
+"""Measurement plumbing on CPU: the PMC summariser (scripts/pmc_summary.py)
+and the committed counter summary that bench.py's roofline objects read."""
+import csv
+import importlib.util
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _pmc_summary():
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(ROOT, "scripts", "pmc_summary.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _write_counters(d, rows):
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "run_counter_collection.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for r in rows:
+            w.writerow(r)
+
+
+def test_sq_summary_per_iteration(tmp_path):
+    """VALU/SALU counts per launch per kernel; the per-iteration total leaves out
+    the once-per-renderer k_primary."""
+    m = _pmc_summary()
+    gf = "void pt::k_trace_gf<64, 9, false>(pt::KParams, int, int)"
+    rows = [
+        {"Kernel_Name": gf, "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": 100.0},
+        {"Kernel_Name": gf, "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": 300.0},
+        {"Kernel_Name": gf, "Counter_Name": "SQ_INSTS_SALU", "Counter_Value": 50.0},
+        {"Kernel_Name": gf, "Counter_Name": "SQ_INSTS_SALU", "Counter_Value": 70.0},
+        {"Kernel_Name": "void pt::k_primary<2>(pt::KParams)", "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": 1e6},
+        {"Kernel_Name": "void pt::k_primary<2>(pt::KParams)", "Counter_Name": "SQ_INSTS_SALU", "Counter_Value": 1e6},
+        {"Kernel_Name": "pt::k_scan(pt::KParams, int)", "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": 20.0},
+        {"Kernel_Name": "pt::k_scan(pt::KParams, int)", "Counter_Name": "SQ_INSTS_SALU", "Counter_Value": 10.0},
+    ]
+    _write_counters(str(tmp_path / "sq"), rows)
+    out = str(tmp_path / "pmc.json")
+    with open(out, "w") as f:      # an existing FETCH/WRITE entry for the key survives
+        json.dump({"w": {"k_trace_gf": {"hbm_bytes_per_launch": 5.0}}}, f)
+    m.main_sq("w", str(tmp_path / "sq"), 2, "_sq", out)
+    d = json.load(open(out))["w"]
+    assert d["k_trace_gf"]["hbm_bytes_per_launch"] == 5.0
+    sq = d["_sq"]
+    assert sq["kernels"]["k_trace_gf"]["valu_insts_per_launch"] == 200.0
+    assert sq["kernels"]["k_trace_gf"]["launches"] == 2
+    assert sq["valu_insts_per_iteration"] == (400.0 + 20.0) / 2
+    assert sq["salu_insts_per_iteration"] == (120.0 + 10.0) / 2
+
+
+def test_committed_pmc_summary_has_bench_keys():
+    """bench.py's roofline.traffic and issue_roofline read these entries for the
+    default workload (both accelerations)."""
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_latest.json")))
+    for accel, kern in (("grid_fast", "k_trace_gf"), ("bvh", "k_trace_bvh")):
+        e = d[f"{accel}_100000_1280x1024_b8"]
+        assert e[kern]["hbm_bytes_per_launch"] > 0
+        assert e["_sq"]["valu_insts_per_iteration"] > 0
+        assert e["_sq_p1"]["kernels"][kern]["valu_insts_per_launch"] > 0
