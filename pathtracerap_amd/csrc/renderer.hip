@@ -635,7 +635,10 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
                                              GetM get, int nh, float tmin, float win, int& tri) {
     int cnt = 0;
     int ulx = 1023, uly = 1023, ulz = 1023, uhx = 0, uhy = 0, uhz = 0;
-#define PT_CERT_FAIL(r) { if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 32 + (r) + kMaxBounceCounters, 1ull); return false; }
+    // A failed condition clears `ok` instead of returning: the computation after it is
+    // harmless, and one exit saves the scalar exec-mask work of eight divergent returns.
+    bool ok = true;
+#define PT_CERT_FAIL(r) { if (PT_TRACE_STATS && (p.debug & 4) && ok) atomicAdd(p.segments + 32 + (r) + kMaxBounceCounters, 1ull); ok = false; }
 #if PT_CERT_FILTER
     // U is the union over the members the walk might enter no later than B*
     // (the minimum-t members' union box); members whose box it provably enters
@@ -776,7 +779,7 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
     if (!(t_box + te < tmin + win)) PT_CERT_FAIL(7)
 #undef PT_CERT_FAIL
     tri = bi;
-    return true;
+    return ok;
 }
 
 template <int CAP, class GetM, bool CERT = true, bool STRICT = false>
