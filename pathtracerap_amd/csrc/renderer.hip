@@ -761,7 +761,9 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
                 const float q = (pp[b] + dd[b] * sin - M.bbox[b]) * M.ivw[b];
                 const float f = floorf(q);
                 if (!(fminf(q - f, f + 1.0f - q) * M.vw[b] > M.cslack[b] + absr(dd[b]) * err)) PT_CERT_FAIL(5)
-                va[b] = (int)f;
+                // clamped: after a failed condition (no early return any more) f may be
+                // huge or NaN; indices outside 0..1023 match no member either way
+                va[b] = (int)fminf(fmaxf(f, -1.0f), 1024.0f);
             }
         }
         te = sin + err;
@@ -1869,9 +1871,13 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
-                if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
-                const f3 pt = o + d * t_box;
-                if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
+                // the grid's box test and entry check as one condition (one divergent `continue`)
+                float tb = 0.0f;
+                const bool boxhit = slab_ref(M.bbox, o, d, inv, tb);
+                const f3 pt = o + d * tb;
+                if (!(boxhit & !((pt.x - M.bbox[0]) < -kEps) & !((pt.y - M.bbox[1]) < -kEps) &
+                      !((pt.z - M.bbox[2]) < -kEps))) continue;
+                t_box = tb;
                 ninv = node_inv(inv);
                 G = mk3((M.vw[0] + M.cslack[0]) * absr(ninv.x), (M.vw[1] + M.cslack[1]) * absr(ninv.y),
                         (M.vw[2] + M.cslack[2]) * absr(ninv.z));
