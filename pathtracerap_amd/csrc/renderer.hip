@@ -2899,7 +2899,6 @@ int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
     const dim3 grid((unsigned)kp.nblocks + 8u);
     for (int b = 0; b < passes; b++) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
         if (b > 0 && split_trace) {
             if (k.order) {
                 const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
@@ -2907,6 +2906,8 @@ int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
                 hipLaunchKernelGGL(k_sort_prefix, dim3(1), dim3(kSortWG), 0, st, k);
                 hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
             }
+            // the trace pair brackets the trace launches only (not the sort kernels)
+            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             launchTrace(k, st, b);
             PT_HIP(hipGetLastError());
             if (profiling) {
@@ -2916,6 +2917,7 @@ int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
             }
             launchBounce(k, st, false, grid, iter, b, kAccelHitBuffer);
         } else {
+            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             launchBounce(k, st, b == 0, grid, iter, b, cfg.accel);
         }
         PT_HIP(hipGetLastError());

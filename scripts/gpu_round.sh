@@ -13,7 +13,7 @@ cp profiles/pmc_latest.json gpurun_out/pmc_latest.json
 for ACC in grid_fast bvh; do
   B="bench.py --accel $ACC --alt-accel= --steps 8 --warmup 1 --no-cpu-baseline --no-profile"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$ACC -o run --output-format csv -- python3 $B > gpurun_out/prof_$ACC.log 2>&1 || { tail -20 gpurun_out/prof_$ACC.log; exit 1; }
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1_$ACC -o run --output-format csv -- python3 $B --pipelines 1 > gpurun_out/prof1_$ACC.log 2>&1 || { tail -20 gpurun_out/prof1_$ACC.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1_$ACC -o run --output-format csv -- python3 bench.py --accel $ACC --alt-accel= --steps 32 --warmup 2 --no-cpu-baseline --no-profile --pipelines 1 > gpurun_out/prof1_$ACC.log 2>&1 || { tail -20 gpurun_out/prof1_$ACC.log; exit 1; }
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$ACC -o run --output-format csv -- python3 $B --pipelines 1 > gpurun_out/pmc_fetch_$ACC.log 2>&1 || { tail -20 gpurun_out/pmc_fetch_$ACC.log; exit 1; }
   timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$ACC -o run --output-format csv -- python3 $B --pipelines 1 > gpurun_out/pmc_write_$ACC.log 2>&1 || { tail -20 gpurun_out/pmc_write_$ACC.log; exit 1; }
   python3 scripts/pmc_summary.py ${ACC}_100000_1280x1024_b8 gpurun_out/pmc_fetch_$ACC gpurun_out/pmc_write_$ACC gpurun_out/pmc_latest.json > /dev/null || exit 1
