@@ -10,7 +10,7 @@
  *   pt_scene_load_obj        <- Scene::loadAndProcessMeshFile        Scene.cpp:226-238
  *   pt_scene_add_mesh        <- Scene::processMesh                   Scene.cpp:264-291
  *   pt_scene_add_model       <- Model setup in Scene::Scene          Scene.cpp:32-42 (x11)
- *   pt_scene_build           <- Scene::addMeshesToGrid               Scene.cpp:318-396
+ *   pt_scene_build           <- Scene::addMeshesToGrid               Scene.cpp:318-396 (+ the per-mesh BLAS)
  *   pt_renderer_allocate_on_gpu <- Renderer::allocateOnGPU           Renderer.cpp:65-130, Renderer.h:371
  *   pt_renderer_clear_image  <- initImageKernel                      Renderer.cpp:557-565
  *   pt_renderer_render_loop  <- Renderer::renderLoop                 Renderer.cpp:567-648, Renderer.h:372
@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 3
+#define PT_ABI_VERSION 4
 
 /* Primitive.h:213-222 Material::MaterialType */
 enum {
@@ -57,15 +57,17 @@ typedef struct pt_render_config {
     int width, height;        /* RESOLUTION_X/Y (Config.h:12-13), default 1000 x 800 */
     int iterations;           /* ITER (Config.h:19), default 500: used by render_image / pt_render */
     int max_bounces;          /* remaining_bounces (Renderer.cpp:550), default 5 */
-    int accel;                /* PT_ACCEL_*, default PT_ACCEL_GRID */
+    int accel;                /* PT_ACCEL_*, default PT_ACCEL_GRID_FAST (the reference grid's results, bit for bit) */
     int grid[3];              /* GRID_X/Y/Z (Config.h:8-10), default 25^3 */
     int tail_drop;            /* 1: replicate the reference's ceil(n/32) launch truncation */
     double cam[3];            /* camera origin (Renderer.cpp:528), default (0,0,920) */
     double plane_z;           /* image plane z (Renderer.cpp:543), default 900 */
     double plane_x0, plane_y0, plane_w, plane_h;  /* Renderer.cpp:538-542: -10,-4,20,16 */
     int block;                /* bounce-kernel workgroup = compaction chunk: 64 (default), 128 or 256 */
-    int pipelines;            /* iterations in flight on their own HIP streams, 1..16 (default 8); results
-                                 are identical for every value (contributions merge in iteration order) */
+    int pipelines;            /* iterations in flight on their own HIP streams, 1..16 (default 16); results
+                                 are identical for every value (contributions merge in iteration order).
+                                 Loading the library sets GPU_MAX_HW_QUEUES=16 (one hardware queue per
+                                 pipeline stream) unless the process already set it */
     int ray_sort;             /* ray sort before each persistent trace: -1 auto (key 7 for grid_fast and bvh),
                                  0 off, 1..8 key layout; claim order only, results identical */
 } pt_render_config;
@@ -85,6 +87,8 @@ int pt_scene_add_mesh(pt_scene *s, const float *pos, const float *nrm, int nv,
                       const int *tris, int nt);                        /* -> mesh index */
 int pt_scene_add_model(pt_scene *s, int mesh, const float scale[3], const float rot_deg[3],
                        const float translate[3], int material, const float color[3]); /* -> model index */
+/* with_bvh: also build the per-mesh BLAS (needed by PT_ACCEL_GRID_FAST and PT_ACCEL_BVH;
+ * pt_renderer_allocate_on_gpu adds it on demand to a scene built without it). */
 int pt_scene_build(pt_scene *s, const int grid[3], int with_bvh);
 /* counts[9] = nv nt nmesh nmodel ngrid nvox npv nbvh_nodes nbvh_refs */
 int pt_scene_counts(const pt_scene *s, int counts[9]);
@@ -112,7 +116,9 @@ pt_renderer *pt_renderer_create(const pt_render_config *cfg);
 int pt_renderer_set_stream(pt_renderer *r, void *hip_stream);
 /* Accumulate into caller-owned device memory (W*H*3 floats) instead of an internal buffer. */
 int pt_renderer_bind_image(pt_renderer *r, float *device_rgb);
+/* For PT_ACCEL_GRID_FAST / PT_ACCEL_BVH a scene built without the BLAS gets it here (once). */
 int pt_renderer_allocate_on_gpu(pt_renderer *r, const pt_scene *s);
+/* Zeroes the accumulator and the trace-fault counter (a new render starts). */
 int pt_renderer_clear_image(pt_renderer *r);
 /* Enqueue iterations [first_iter, first_iter + n_iters) (asynchronous). */
 int pt_renderer_render_loop(pt_renderer *r, int first_iter, int n_iters);
@@ -122,8 +128,8 @@ int pt_renderer_render_image(pt_renderer *r, const char *bmp_path, int iteration
 /* Ray segments shaded so far (sum over bounces of live rays). */
 long long pt_renderer_segments(pt_renderer *r);
 /* Persistent-trace waves that hit their iteration cap and left rays untraced since
- * allocate_on_gpu (0 in a correct run; -1 on error).  Non-zero makes
- * pt_renderer_synchronize / read_image / render_image fail: the image is invalid. */
+ * allocate_on_gpu or the last clear_image (0 in a correct run; -1 on error).  Non-zero
+ * makes pt_renderer_synchronize / read_image / render_image fail: the image is invalid. */
 long long pt_renderer_trace_faults(pt_renderer *r);
 /* out[b] = live rays entering bounce b, summed over the iterations rendered (b < n, n <= 64 useful). */
 int pt_renderer_segments_per_bounce(pt_renderer *r, long long *out, int n);
@@ -133,8 +139,9 @@ int pt_renderer_pipelines(pt_renderer *r);
 /* stats[0..6] = secondary-bounce ms, scan ms, primary ms, secondary-bounce launches,
  * scan launches, first-bounce ms, first-bounce launches (HIP events; resets). */
 int pt_renderer_kernel_stats(pt_renderer *r, double stats[7]);
-/* Same, n values: stats[7..8] = persistent-trace ms, launches (ACCEL_BVH splits each
- * secondary bounce into k_trace_bvh + a shading pass; stats[0] is then the shading pass). */
+/* Same, n values: stats[7..8] = persistent-trace ms, launches (grid_fast / bvh split each
+ * secondary bounce into a persistent trace + a shading pass; stats[0] is then the shading
+ * pass); stats[9..10] = ray-sort ms, sort passes (k_sort_hist + prefix + scatter). */
 int pt_renderer_kernel_stats_ex(pt_renderer *r, double *stats, int n);
 /* Test hooks: primary-hit cache and batch intersection (host arrays). */
 int pt_renderer_primary_hits(pt_renderer *r, float *dist, float *normal, int *model);

@@ -32,6 +32,9 @@ _LIB_PATH = os.environ.get("PT_LIB_PATH") or os.path.join(_HERE, "libpathtracer_
 ACCEL_GRID = 0
 ACCEL_BVH = 1
 ACCEL_GRID_FAST = 2
+# renderer.h: segments[] slots after the per-bounce counters, as segments_per_bounce indices
+_MAX_BOUNCE_COUNTERS = 64
+_DEFERRED_SLOT = 50 + _MAX_BOUNCE_COUNTERS - 1     # kDeferredRayCounter
 # Primitive.h:213-222
 MATERIALS = {"DIFFUSE": 0, "SPECULAR": 1, "REFLECTIVE": 2, "REFRACTIVE": 3,
              "EMISSIVE": 4, "COAT": 5, "METAL": 6}
@@ -146,7 +149,7 @@ class RenderConfig:
     height: int = 800
     iterations: int = 500
     max_bounces: int = 5
-    accel: int = ACCEL_GRID
+    accel: int = ACCEL_GRID_FAST   # the reference grid's results, bit for bit (ACCEL_GRID: its list-walking DDA)
     grid: tuple = (25, 25, 25)
     tail_drop: int = 0
     cam: tuple = (0.0, 0.0, 920.0)
@@ -156,7 +159,7 @@ class RenderConfig:
     plane_w: float = 20.0
     plane_h: float = 16.0
     block: int = 64
-    pipelines: int = 8    # iterations in flight (own HIP streams); results identical for any value
+    pipelines: int = 16   # iterations in flight (own HIP streams); results identical for any value
     ray_sort: int = -1    # ray sort key before each persistent trace (-1 auto, 0 off); results identical
 
     def c(self) -> _Cfg:
@@ -214,7 +217,9 @@ class Scene:
         t = np.array(translate, np.float32); c = np.array(color, np.float32)
         return _err(lib().pt_scene_add_model(self._h, int(mesh), _fp(s), _fp(r), _fp(t), mt, _fp(c)), "addModel")
 
-    def build(self, grid=(25, 25, 25), bvh: bool = False) -> None:
+    def build(self, grid=(25, 25, 25), bvh: bool = True) -> None:
+        """addMeshesToGrid (grid) + the per-mesh BLAS that ACCEL_GRID_FAST / ACCEL_BVH
+        traverse (``bvh=False``: grid only; allocateOnGPU then adds the BLAS on demand)."""
         g = (ctypes.c_int * 3)(*grid)
         _err(lib().pt_scene_build(self._h, g, 1 if bvh else 0), "build")
 
@@ -341,12 +346,18 @@ class Renderer:
         _err(lib().pt_renderer_set_profiling(self._h, 1 if on else 0), "set_profiling")
 
     def kernel_stats(self) -> dict:
-        st = (ctypes.c_double * 9)()
-        _err(lib().pt_renderer_kernel_stats_ex(self._h, st, 9), "kernel_stats")
+        st = (ctypes.c_double * 11)()
+        _err(lib().pt_renderer_kernel_stats_ex(self._h, st, 11), "kernel_stats")
         return dict(bounce_ms=st[0], scan_ms=st[1], primary_ms=st[2],
                     bounce_launches=int(st[3]), scan_launches=int(st[4]),
                     first_ms=st[5], first_launches=int(st[6]),
-                    trace_ms=st[7], trace_launches=int(st[8]))
+                    trace_ms=st[7], trace_launches=int(st[8]),
+                    sort_ms=st[9], sort_launches=int(st[10]))
+
+    def deferred_rays(self) -> int:
+        """Rays k_trace_deferred traced since allocateOnGPU (grid_fast hit sets beyond
+        the overflow pool, or undecided walks beyond the hand-on records' room)."""
+        return self.segments_per_bounce(_DEFERRED_SLOT + 1)[_DEFERRED_SLOT]
 
     def primary_hits(self):
         n = self.cfg.width * self.cfg.height
@@ -379,7 +390,7 @@ class Renderer:
 
 
 def render(scene_config: str, cfg: RenderConfig | None = None, bmp_out: str | None = "Render.bmp") -> None:
-    """main.cpp:11-27 equivalent."""
-    c = (cfg or RenderConfig()).c()
-    _err(lib().pt_render(os.fsencode(scene_config), ctypes.byref(c),
-                         os.fsencode(bmp_out) if bmp_out else None), "render")
+    """main.cpp:11-27 equivalent.  ``cfg=None``: the library's defaults
+    (pt_default_config) overlaid with the scene file's RENDER block."""
+    c = ctypes.byref(cfg.c()) if cfg is not None else None
+    _err(lib().pt_render(os.fsencode(scene_config), c, os.fsencode(bmp_out) if bmp_out else None), "render")

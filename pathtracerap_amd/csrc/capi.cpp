@@ -1,4 +1,5 @@
 // capi.cpp -- extern "C" boundary (include/pathtracer_amd.h).
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -10,6 +11,17 @@ struct pt_scene { pt::Scene s; };
 struct pt_renderer { pt::Renderer* r; };
 
 static thread_local std::string g_err;
+
+// Iterations in flight run on their own HIP streams (pt_render_config.pipelines,
+// default 16); HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default
+// 4), so with the default several pipelines share a queue and serialise
+// (DESIGN.md "Results": 8 pipelines on 4 queues ran 1570 Mrays/s at configs[1]).  The variable is read once, when
+// the HIP runtime initialises: set it at load time unless the process already
+// chose a value.  (A process whose HIP runtime started before this library was
+// loaded keeps its own setting.)
+__attribute__((constructor)) static void pt_default_hw_queues() {
+    setenv("GPU_MAX_HW_QUEUES", "16", /*overwrite=*/0);
+}
 
 static int set_err(const std::string& m) { g_err = m; return -1; }
 
@@ -200,6 +212,13 @@ int pt_renderer_set_stream(pt_renderer* r, void* st) { R_CALL(r->r->setStream((h
 int pt_renderer_bind_image(pt_renderer* r, float* d) { R_CALL(r->r->bindImage(d)); }
 int pt_renderer_allocate_on_gpu(pt_renderer* r, const pt_scene* s) {
     if (!s) return set_err("null scene");
+    if (!r || !r->r) return set_err("null renderer");
+    if (r->r->cfg.accel != PT_ACCEL_GRID && s->s.built && s->s.bvh_nodes.empty()) {
+        // grid_fast / bvh traverse the per-mesh BLAS: a scene built grid-only gets it
+        // here, once (the scene's grid tables are rebuilt identically alongside)
+        pt::Scene& S = const_cast<pt_scene*>(s)->s;
+        if (S.ensureBvh() < 0) return set_err(S.last_error);
+    }
     R_CALL(r->r->allocateOnGPU(s->s));
 }
 int pt_renderer_clear_image(pt_renderer* r) { R_CALL(r->r->clearImage()); }
@@ -245,9 +264,10 @@ int pt_renderer_kernel_stats_ex(pt_renderer* r, double* st, int n) {
     if (!r || !r->r || !st || n < 0) return set_err("bad arguments");
     pt::KernelStats k;
     if (r->r->kernelStats(&k) < 0) return set_err(r->r->last_error);
-    const double v[9] = {k.bounce_ms, k.scan_ms, k.primary_ms, (double)k.bounce_launches, (double)k.scan_launches,
-                         k.first_ms, (double)k.first_launches, k.trace_ms, (double)k.trace_launches};
-    for (int i = 0; i < n; i++) st[i] = i < 9 ? v[i] : 0.0;
+    const double v[11] = {k.bounce_ms, k.scan_ms, k.primary_ms, (double)k.bounce_launches, (double)k.scan_launches,
+                          k.first_ms, (double)k.first_launches, k.trace_ms, (double)k.trace_launches,
+                          k.sort_ms, (double)k.sort_launches};
+    for (int i = 0; i < n; i++) st[i] = i < 11 ? v[i] : 0.0;
     return 0;
 }
 int pt_renderer_primary_hits(pt_renderer* r, float* d, float* n, int* m) {
@@ -278,7 +298,7 @@ int pt_render(const char* scene_config, const pt_render_config* cfg, const char*
     if (!s) return -1;
     int rc = pt_scene_load_config(s, scene_config);
     if (rc >= 0) rc = pt_scene_apply_settings(s, &c);
-    if (rc >= 0) rc = pt_scene_build(s, c.grid, c.accel != PT_ACCEL_GRID);
+    if (rc >= 0) rc = pt_scene_build(s, c.grid, c.accel != PT_ACCEL_GRID ? 1 : 0);
     pt_renderer* r = rc >= 0 ? pt_renderer_create(&c) : nullptr;
     if (rc >= 0 && !r) rc = -1;
     if (rc >= 0) rc = pt_renderer_allocate_on_gpu(r, s);

@@ -1,7 +1,11 @@
 // main.cpp -- command-line renderer (the reference's main.cpp:11-27):
 // load a scene, allocate on the GPU, run the render loop, write Render.bmp.
 //
-//   pathtracer_amd <scene.txt> [out.bmp] [--res W H] [--iter N] [--bounces B] [--bvh]
+//   pathtracer_amd <scene.txt> [out.bmp] [--res W H] [--iter N] [--bounces B] [--grid|--grid-fast|--bvh]
+//                  [--pipelines P]
+//
+// Default: PT_ACCEL_GRID_FAST (the reference grid's image, bit for bit) with 16
+// iterations in flight, each on its own HIP stream and hardware queue.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -10,8 +14,12 @@
 #include "../../include/pathtracer_amd.h"
 
 int main(int argc, char** argv) {
+    // one hardware queue per pipeline stream; read once when the HIP runtime starts
+    // (the library sets the same default when it loads; an explicit choice wins)
+    setenv("GPU_MAX_HW_QUEUES", "16", /*overwrite=*/0);
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s scene.txt [out.bmp] [--res W H] [--iter N] [--bounces B] [--bvh|--grid-fast]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s scene.txt [out.bmp] [--res W H] [--iter N] [--bounces B] "
+                             "[--grid|--grid-fast|--bvh] [--pipelines P]\n", argv[0]);
         return 2;
     }
     pt_render_config cfg;
@@ -26,6 +34,8 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--bounces") && i + 1 < argc) cfg.max_bounces = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--bvh")) cfg.accel = PT_ACCEL_BVH;
         else if (!std::strcmp(argv[i], "--grid-fast")) cfg.accel = PT_ACCEL_GRID_FAST;
+        else if (!std::strcmp(argv[i], "--grid")) cfg.accel = PT_ACCEL_GRID;
+        else if (!std::strcmp(argv[i], "--pipelines") && i + 1 < argc) cfg.pipelines = std::atoi(argv[++i]);
         else out = argv[i];
     }
     if (pt_scene_build(s, cfg.grid, cfg.accel != PT_ACCEL_GRID) < 0) { std::fprintf(stderr, "%s\n", pt_last_error()); return 1; }

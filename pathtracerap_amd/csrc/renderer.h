@@ -22,12 +22,12 @@ struct RenderConfig {            // Config.h + generateRaysKernel constants, at 
     int width = 1000, height = 800;       // RESOLUTION_X/Y
     int iterations = 500;                 // ITER
     int max_bounces = 5;                  // Renderer.cpp:550
-    int accel = ACCEL_GRID;
+    int accel = ACCEL_GRID_FAST;          // the reference grid's results, bit for bit, through the BLAS
     int grid[3] = {25, 25, 25};           // GRID_X/Y/Z
     int tail_drop = 0;                    // replicate ceil(n/32) launch truncation (Renderer.cpp:573)
     int block = 64;                       // bounce-kernel workgroup size = compaction chunk (64/128/256)
     int ray_sort = -1;                    // -1 auto (grid_fast: key 7), 0 off, 1..8 key layout (k_sort_hist)
-    int pipelines = 8;                    // iterations in flight on their own HIP streams (1..kMaxPipes)
+    int pipelines = 16;                   // iterations in flight on their own HIP streams (1..kMaxPipes)
     double cam[3] = {0.0, 0.0, 920.0};    // Renderer.cpp:528
     double plane_z = 900.0;               // Renderer.cpp:543
     double plane_x0 = -10.0, plane_y0 = -4.0, plane_w = 20.0, plane_h = 16.0;  // Renderer.cpp:538-542
@@ -102,9 +102,14 @@ constexpr int kDiagCounters = 64;        // diagnostic counters after the per-bo
 // segments[] slot counting persistent-trace waves that hit trace_iter_cap and left
 // rays untraced (their hit records are stale): any non-zero value invalidates the image
 constexpr int kTraceFaultCounter = 7 + kMaxBounceCounters;
+// segments[] slot counting rays k_trace_deferred traced (grid_fast hit sets that
+// outgrew the overflow pool, or walks past the hand-on records' room); every build
+constexpr int kDeferredRayCounter = 50 + kMaxBounceCounters;
 
 struct KernelStats {
     double bounce_ms = 0, scan_ms = 0, primary_ms = 0, first_ms = 0, trace_ms = 0;
+    double sort_ms = 0;                  // ray sort before each persistent trace (k_sort_hist/prefix/scatter)
+    long long sort_launches = 0;
     long long bounce_launches = 0, scan_launches = 0, first_launches = 0;   // bounce_* = secondary bounces
     long long trace_launches = 0;        // k_trace_bvh (split trace/shade); bounce_* is then the shading pass
 };
@@ -165,7 +170,7 @@ private:
     float* ext_image = nullptr;
     bool profiling = false;
     std::vector<void*> allocs;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events, trace_events;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events, trace_events, sort_events;
     bool split_trace = false;        // persistent k_trace_bvh / k_trace_gf + shading pass
     int trace_blocks = 0;
     int gf_flags = 9;                // k_trace_gf variant: 1 LDS model records, 8 phase scheduling

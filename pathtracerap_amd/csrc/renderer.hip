@@ -2149,6 +2149,8 @@ __global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
     const int cnt = *p.defer_count;
     if ((PT_TRACE_STATS && (p.debug & 16)) && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(p.segments + 14 + kMaxBounceCounters, (unsigned long long)cnt);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && cnt > 0)      // every build: which route the rays took
+        atomicAdd(p.segments + kDeferredRayCounter, (unsigned long long)cnt);
     for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
         const int j = p.defer_slots[q];
         const int src = slot_source(p, j);
@@ -2792,6 +2794,9 @@ int Renderer::clearImage() {
     const size_t n = (size_t)cfg.width * cfg.height * 3;
     hipLaunchKernelGGL(k_zero, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, kp.image, n);
     PT_HIP(hipGetLastError());
+    // a fault invalidated the image it was counted against; the cleared image starts
+    // a new render, so later checks report only faults of renders after this point
+    PT_HIP(hipMemsetAsync(kp.segments + kTraceFaultCounter, 0, sizeof(unsigned long long), stream));
     return 0;
 }
 
@@ -2809,25 +2814,28 @@ int Renderer::launchPrimary() {
 void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
+        // model records in LDS: the variant asks for them (gf_flags & 1, cleared by
+        // allocateOnGPU when the scene has more than kLdsModels models)
+        const bool lds = (gf_flags & 1) && k.nmodels <= kLdsModels;
         switch (gf_flags) {
             case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b, 0); break;
             case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b, 0); break;
-            case 8: hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0); break;
             case 12: hipLaunchKernelGGL((k_trace_gf<64, 12>), g, t, 0, st, k, b, 0); break;
             case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b, 0); break;
-            default:                         // 9; 8 when the model records do not fit LDS; | 16: walks in place
+            default:                         // 9 and 8 (more models than LDS holds): certificate-only main
+                                             // launch with walk hand-ons, else (| 16) walks in place
                 if (k.cont_wcap > 0) {
-                    if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
+                    if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
                     else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
                 } else {
-                    if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 25>), g, t, 0, st, k, b, 0);
+                    if (lds) hipLaunchKernelGGL((k_trace_gf<64, 25>), g, t, 0, st, k, b, 0);
                     else hipLaunchKernelGGL((k_trace_gf<64, 24>), g, t, 0, st, k, b, 0);
                 }
                 break;
         }
         for (int l = 1; (k.drain_dump > 0 && l <= k.drain_levels) || (k.cont_wcap > 0 && l == 1); l++) {
             // the rays handed on (drain continuations; walk hand-ons go to level 1), packed
-            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b, l);
+            if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b, l);
             else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b, l);
         }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
@@ -2901,10 +2909,12 @@ int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (b > 0 && split_trace) {
             if (k.order) {
+                if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
                 const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
                 hipLaunchKernelGGL(k_sort_hist, sg, dim3(kSortWG), 0, st, k, b);
                 hipLaunchKernelGGL(k_sort_prefix, dim3(1), dim3(kSortWG), 0, st, k);
                 hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
+                if (profiling) { hipEventRecord(e1, st); sort_events.push_back({e0, e1}); e0 = e1 = nullptr; }
             }
             // the trace pair brackets the trace launches only (not the sort kernels)
             if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
@@ -3089,6 +3099,14 @@ int Renderer::kernelStats(KernelStats* out) {
         hipEventDestroy(ev.first); hipEventDestroy(ev.second);
     }
     trace_events.clear();
+    for (auto& ev : sort_events) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev.first, ev.second);
+        stats.sort_ms += ms;
+        stats.sort_launches++;
+        hipEventDestroy(ev.first); hipEventDestroy(ev.second);
+    }
+    sort_events.clear();
     for (auto& ev : scan_events) {
         float ms = 0;
         hipEventElapsedTime(&ms, ev.first, ev.second);
@@ -3234,7 +3252,9 @@ void Renderer::free() {
     for (auto& ev : first_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto& ev : scan_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     for (auto& ev : trace_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
+    for (auto& ev : sort_events) { hipEventDestroy(ev.first); hipEventDestroy(ev.second); }
     trace_events.clear();
+    sort_events.clear();
     bounce_events.clear();
     first_events.clear();
     scan_events.clear();

@@ -718,4 +718,11 @@ int Scene::build(const int gd[3], bool with_bvh) {
     return 0;
 }
 
+int Scene::ensureBvh() {
+    if (!built) { last_error = "scene not built (call build first)"; return -1; }
+    if (!bvh_nodes.empty()) return 0;
+    const int gd[3] = {grid_dim[0], grid_dim[1], grid_dim[2]};
+    return build(gd, true);        // the same grid again (deterministic), plus every mesh's BLAS
+}
+
 }  // namespace pt

@@ -49,7 +49,7 @@ struct Grid {                                           // Primitive.h:272-282
 struct RenderSettings {                                 // Config.h constants, runtime
     int width = 1000, height = 800, iterations = 500, max_bounces = 5;
     int grid[3] = {25, 25, 25};
-    int accel = ACCEL_GRID;
+    int accel = ACCEL_GRID_FAST;
     bool has_width = false, has_iterations = false, has_bounces = false, has_accel = false;
 };
 
@@ -69,6 +69,9 @@ public:
                  const float translate[3], int material_type, const float color[3]);
     // addMeshesToGrid (Scene.cpp:318-396) + device tables.  `grid_dim` = GRID_X/Y/Z.
     int build(const int grid_dim[3], bool with_bvh);
+    // The BLAS on demand: Renderer::allocateOnGPU calls this for the accels that
+    // traverse it (grid_fast, bvh) when the scene was built grid-only.
+    int ensureBvh();
 
     // Scene.h:30-36
     std::vector<Model> models;

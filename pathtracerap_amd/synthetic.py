@@ -132,3 +132,30 @@ def diffuse_scene(out_dir: str, ntri: int = 100_000, seed: int = 0, width: int =
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
     return path
+
+
+# Models of diffuse_scene, in the order its MESH blocks add them:
+# (mesh, translate, rotate, scale, material, color); metallic swaps in the second pair.
+_MODELS = [
+    ("room", (0, -120, 0), (0, 0, 0), (0.1, 0.1, 0.1), ("DIFFUSE", (0.85, 0.85, 0.85)), None),
+    ("torus", (0, 130, 0), (35, 20, 0), (0.1, 0.1, 0.1), ("DIFFUSE", (0.75, 0.62, 0.40)), ("METAL", (0.90, 0.90, 0.95))),
+    ("light", (0, 870, -50), (0, 0, 0), (0.2, 0.02, 0.2), ("EMISSIVE", (0.99, 0.99, 0.99)), None),
+    ("light", (0, 375, 950), (0, 0, 0), (0.2, 0.2, 0.1), ("EMISSIVE", (0.99, 0.99, 0.99)), None),
+    ("light", (-300, -60, 150), (0, 30, 0), (0.06, 0.06, 0.06), ("DIFFUSE", (0.85, 0.15, 0.12)), ("COAT", (0.15, 0.30, 0.90))),
+]
+
+
+def build_scene(P, ntri: int = 100_000, seed: int = 0, metallic: bool = False, grid=(25, 25, 25), bvh: bool = True):
+    """diffuse_scene's layout built in memory (Scene.addMesh / addModel, no OBJ
+    round trip): for the 10M-triangle configs[4] scene, whose OBJ text would take
+    about a minute to write and parse.  Same meshes, transforms and materials; the
+    vertex coordinates are the float32 values themselves rather than their 6-digit
+    OBJ text, so the geometry differs from diffuse_scene's by that rounding."""
+    s = P.Scene()
+    meshes = {"room": s.addMesh(*room_mesh()), "light": s.addMesh(*light_mesh()),
+              "torus": s.addMesh(*torus_mesh(ntri, seed=seed))}
+    for mesh, tr, rot, sc, mat, alt in _MODELS:
+        name, color = alt if (metallic and alt) else mat
+        s.addModel(meshes[mesh], sc, rot, tr, name, color)
+    s.build(grid=grid, bvh=bvh)
+    return s

@@ -8,7 +8,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-INPUT_DATA = os.path.join(GOLDEN, "input_data")
+INPUT_DATA = os.path.join(ROOT, "scenes", "input_data")
 REF_SCENE = os.path.join(ROOT, "scenes", "reference_scene.txt")
 
 

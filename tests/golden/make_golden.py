@@ -5,7 +5,7 @@ Run once in the build container (the GPU box has no /root/reference):
     python tests/golden/make_golden.py [/root/reference/PathTracerAP]
 
 Writes
-  tests/golden/input_data/{enclosing_box,ceiling_light,blender_monkey}.obj
+  scenes/input_data/{enclosing_box,ceiling_light,blender_monkey}.obj
       -- the reference's own scene inputs (data files, copied verbatim);
   tests/golden/reference_render_1000x800_500.npz
       -- the pixel payload of the reference's committed output image
@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def main(ref=None):
     ref = ref or "/root/reference/PathTracerAP"
     for f in ("enclosing_box.obj", "ceiling_light.obj", "blender_monkey.obj"):
-        shutil.copyfile(os.path.join(ref, "Input data", f), os.path.join(HERE, "input_data", f))
+        shutil.copyfile(os.path.join(ref, "Input data", f), os.path.join(HERE, "..", "..", "scenes", "input_data", f))
     raw = open(os.path.join(ref, "Render.bmp"), "rb").read()
     w, h = struct.unpack("<ii", raw[18:26])
     off = struct.unpack("<I", raw[10:14])[0]

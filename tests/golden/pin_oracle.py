@@ -41,7 +41,7 @@ def compare(ours: np.ndarray, ref: np.ndarray) -> dict:
 
 
 def main(threads=1):
-    sc = O.reference_scene(os.path.join(HERE, "input_data"))
+    sc = O.reference_scene(os.path.join(os.path.dirname(os.path.dirname(HERE)), "scenes", "input_data"))
     cfg = O.RenderConfig(width=1000, height=800, iterations=500, threads=int(threads))
     t = time.time()
     img, seg = O.render(sc, cfg)

@@ -25,17 +25,34 @@ def test_library_exports_every_declared_symbol(pt_mod):
 
 def test_abi_version_and_defaults(pt_mod):
     L = pt_mod.lib()
-    assert L.pt_abi_version() == 3
+    assert L.pt_abi_version() == 4
     c = pt_mod._Cfg()
     L.pt_default_config(ctypes.byref(c))
     # Config.h / generateRaysKernel defaults
     assert (c.width, c.height, c.iterations, c.max_bounces) == (1000, 800, 500, 5)
     assert tuple(c.grid) == (25, 25, 25) and tuple(c.cam) == (0.0, 0.0, 920.0)
     assert (c.plane_x0, c.plane_y0, c.plane_w, c.plane_h, c.plane_z) == (-10.0, -4.0, 20.0, 16.0, 900.0)
+    # the drop-in default is the fast path with the reference's results: grid_fast
+    assert c.accel == pt_mod.ACCEL_GRID_FAST
     # throughput knobs (results identical for every value): the struct tail matches the header
-    assert (c.block, c.pipelines, c.ray_sort) == (64, 8, -1)
+    assert (c.block, c.pipelines, c.ray_sort) == (64, 16, -1)
     py = pt_mod.RenderConfig()
-    assert (py.block, py.pipelines, py.ray_sort) == (c.block, c.pipelines, c.ray_sort)
+    assert (py.accel, py.block, py.pipelines, py.ray_sort) == (c.accel, c.block, c.pipelines, c.ray_sort)
+
+
+def test_library_load_sets_hw_queues_unless_chosen():
+    """Loading libpathtracer_amd.so gives the process one hardware queue per
+    pipeline stream (GPU_MAX_HW_QUEUES=16) unless the variable is already set."""
+    import subprocess
+    import sys
+    code = ("import ctypes; ctypes.CDLL(%r); libc = ctypes.CDLL(None); libc.getenv.restype = ctypes.c_char_p; "
+            "print(libc.getenv(b'GPU_MAX_HW_QUEUES'))") % os.path.join(ROOT, "pathtracerap_amd", "libpathtracer_amd.so")
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.strip() == "b'16'"
+    env["GPU_MAX_HW_QUEUES"] = "4"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.strip() == "b'4'"
 
 
 def test_errors_are_reported_not_crashing(pt_mod):

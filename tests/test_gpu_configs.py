@@ -1,0 +1,197 @@
+"""GPU parity at the BASELINE.json configurations' own sizes (the reference's
+bounce loop, Renderer.cpp:567-648, against the CPU oracle, bit for bit).
+
+* configs[1]: the ~100k-triangle diffuse synthetic scene, 1280x1024, 8 bounces,
+  2 iterations -- the bench workload itself, through the drop-in defaults
+  (grid_fast, 16 pipelines, ray sort, drain continuations, walk hand-ons);
+* north_star target: the 1M-triangle scene, 1280x1024, 8 bounces, 1 iteration;
+* configs[2]: the README render's scene (Scene.cpp:3-224 =
+  scenes/reference_scene.txt) at 2800x2240, 5 bounces, 1 iteration;
+* configs[4]: the 10M-triangle scene, 16 bounces (deep BLAS at the depth cap,
+  dense hit sets): a 64x64 window of the frame against the oracle, plus
+  full-frame properties (no trace faults, finite image, per-bounce ray counts
+  and image equal to the reference grid mode's on a 320x256 frame of the same
+  view);
+* the drop-in entry points with no configuration: pt_render (main.cpp:11-27)
+  and the pathtracer_amd CLI render the reference scene at its own settings
+  (1000x800, ITER 500) byte-identical to the committed oracle render.
+
+The oracle runs on 16 host threads; every case finishes in well under a minute
+on the GPU box.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REF_SCENE, ROOT
+from helpers import assert_bitexact, flat_from_export, oracle_cfg
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+@pytest.fixture(scope="module")
+def synth_dir(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("cfgscenes"))
+
+
+def _gpu_render(P, scene, cfg):
+    r = P.Renderer(cfg)
+    r.allocateOnGPU(scene)
+    r.renderLoop()
+    out = dict(img=r.image(), seg=r.segments(), per_bounce=r.segments_per_bounce(cfg.max_bounces + 1),
+               faults=r.trace_faults(), pipes=r.pipelines())
+    r.free()
+    return out
+
+
+def _oracle_render(O, scene, cfg):
+    img, seg = O.render(flat_from_export(scene.export(), cfg.grid), oracle_cfg(cfg, threads=THREADS))
+    return img, seg
+
+
+def test_configs1_bench_workload_bitexact(gpu, pt_mod, oracle_mod, synth_dir):
+    """configs[1] at full size through the defaults the bench and the drop-in use."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=100_000))
+    s.build()
+    assert s.counts()["nt"] > 99_000
+    cfg = s.apply_settings(P.RenderConfig())
+    cfg.iterations = 2
+    assert (cfg.width, cfg.height, cfg.max_bounces) == (1280, 1024, 8)
+    assert cfg.accel == P.ACCEL_GRID_FAST and cfg.pipelines == 16
+    g = _gpu_render(P, s, cfg)
+    assert g["pipes"] == 16 and g["faults"] == 0
+    oimg, oseg = _oracle_render(O, s, cfg)
+    assert g["seg"] == oseg
+    assert_bitexact(g["img"], oimg, "configs[1] 1280x1024 image")
+
+
+def test_target_1m_triangles_bitexact(gpu, pt_mod, oracle_mod, synth_dir):
+    """north_star target scene (1M-triangle diffuse OBJ) at 1280x1024."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=1_000_000))
+    s.build()
+    assert s.counts()["nt"] > 990_000
+    cfg = P.RenderConfig(width=1280, height=1024, iterations=1, max_bounces=8)
+    g = _gpu_render(P, s, cfg)
+    assert g["faults"] == 0
+    oimg, oseg = _oracle_render(O, s, cfg)
+    assert g["seg"] == oseg
+    assert_bitexact(g["img"], oimg, "1M-triangle 1280x1024 image")
+
+
+def test_configs2_readme_scene_2800x2240_bitexact(gpu, pt_mod, oracle_mod):
+    """configs[2]: the README render's own scene (metal, coat, diffuse and
+    emissive models of Scene.cpp) at 2800x2240, the reference's 5 bounces."""
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(REF_SCENE)
+    s.build()
+    cfg = s.apply_settings(P.RenderConfig())
+    cfg.width, cfg.height, cfg.iterations = 2800, 2240, 1
+    assert cfg.max_bounces == 5
+    g = _gpu_render(P, s, cfg)
+    assert g["faults"] == 0
+    oimg, oseg = _oracle_render(O, s, cfg)
+    assert g["seg"] == oseg
+    assert_bitexact(g["img"], oimg, "configs[2] 2800x2240 image")
+
+
+@pytest.fixture(scope="module")
+def scene_10m(pt_mod):
+    from pathtracerap_amd import synthetic
+    return synthetic.build_scene(pt_mod, ntri=10_000_000)
+
+
+def _bvh_depth(scene):
+    """Deepest level of the binary BLAS (root = 1), by a vectorised walk."""
+    b = scene.export_bvh()
+    nodes = b["nodes"].view(np.int32)
+    depth, frontier = 0, np.unique(b["roots"][b["roots"] >= 0])
+    while len(frontier):
+        depth += 1
+        n = nodes[frontier]
+        # BvhNode: (lo0.xyz, link0) (hi0.xyz, link1) (lo1.xyz, cnt0) (hi1.xyz, cnt1); cnt 0 = inner child
+        link = np.stack([n[:, 3], n[:, 7]], 1)
+        cnt = np.stack([n[:, 11], n[:, 15]], 1)
+        frontier = link[cnt == 0]
+    return depth
+
+
+def test_configs4_10m_triangles_window_bitexact(gpu, pt_mod, oracle_mod, scene_10m):
+    """configs[4]: 10M triangles, 16 bounces -- a 64x64 window of the 1280x1024
+    frame on the torus ring (plane_x0/plane_w select it) against the oracle."""
+    P, O = pt_mod, oracle_mod
+    s = scene_10m
+    assert s.counts()["nt"] > 9_900_000
+    assert _bvh_depth(s) <= 24          # bvh.cpp kMaxDepth = 23 holds at 10M triangles (node levels incl. the root)
+    cfg = P.RenderConfig(width=64, height=64, iterations=1, max_bounces=16,
+                         plane_x0=5.0, plane_y0=2.5, plane_w=1.0, plane_h=1.0)
+    g = _gpu_render(P, s, cfg)
+    assert g["faults"] == 0
+    oimg, oseg = _oracle_render(O, s, cfg)
+    assert g["seg"] == oseg
+    assert_bitexact(g["img"], oimg, "configs[4] 10M-triangle window")
+    # the window sees the dense mesh (model 1) for most primary rays
+    r = P.Renderer(cfg)
+    r.allocateOnGPU(s)
+    _, _, m = r.primary_hits()
+    r.free()
+    assert (m == 1).mean() > 0.5
+
+
+def test_configs4_10m_triangles_full_frame_properties(gpu, pt_mod, scene_10m):
+    """configs[4] full frame (1280x1024, 16 bounces): no trace faults, a finite
+    image, and rays reaching deep bounces; on a 320x256 frame of the same view
+    the image and every bounce's live-ray count equal the reference grid mode's
+    (list-walking DDA, the literal restatement of Renderer.cpp:238-360)."""
+    P = pt_mod
+    s = scene_10m
+    cfg = P.RenderConfig(width=1280, height=1024, iterations=1, max_bounces=16)
+    g = _gpu_render(P, s, cfg)
+    assert g["faults"] == 0
+    assert np.isfinite(g["img"]).all() and g["img"].sum() > 0
+    pb = g["per_bounce"]
+    assert pb[0] == 1280 * 1024 and pb[8] > 0 and sum(pb) == g["seg"]
+    small = P.RenderConfig(width=320, height=256, iterations=1, max_bounces=16)
+    a = _gpu_render(P, s, small)
+    small.accel = P.ACCEL_GRID
+    b = _gpu_render(P, s, small)
+    assert a["faults"] == 0 and b["faults"] == 0
+    assert a["per_bounce"] == b["per_bounce"]
+    assert_bitexact(a["img"], b["img"], "grid_fast vs grid, 10M triangles")
+
+
+def _oracle_bmp_payload():
+    return np.load(os.path.join(GOLDEN, "oracle_render_1000x800_500.npz"))["bgr"]
+
+
+def _bmp_payload(path):
+    raw = open(path, "rb").read()
+    assert len(raw) == 54 + 3 * 1000 * 800
+    return np.frombuffer(raw[54:], np.uint8).reshape(800, 1000, 3)
+
+
+def test_pt_render_defaults_equal_oracle(gpu, pt_mod, tmp_path):
+    """pt_render (main.cpp:11-27) with no configuration: the reference scene at
+    its own settings through the default path (grid_fast, 16 pipelines) writes
+    the oracle's 500-iteration Render.bmp byte for byte."""
+    out = tmp_path / "Render.bmp"
+    pt_mod.render(REF_SCENE, None, str(out))
+    assert np.array_equal(_bmp_payload(out), _oracle_bmp_payload())
+
+
+def test_cli_defaults_equal_oracle(gpu, pt_mod, tmp_path):
+    """The pathtracer_amd CLI with no flags: same bytes."""
+    exe = os.path.join(ROOT, "pathtracerap_amd", "pathtracer_amd")
+    out = tmp_path / "Render.bmp"
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    p = subprocess.run([exe, REF_SCENE, str(out)], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr
+    assert "Mrays/s" in p.stdout
+    assert np.array_equal(_bmp_payload(out), _oracle_bmp_payload())

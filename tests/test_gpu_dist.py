@@ -1,0 +1,91 @@
+"""The sample-sharded multi-rank path on the HIP renderer (dist.render_sharded
+with its default GPU branch): two gloo ranks share the one GPU, each renders
+its iteration range (Renderer.cpp:582-644: iterations are independent) into its
+own torch accumulator on the caller's stream, and the all-reduced image equals
+the single-rank render up to fp32 summation order (rtol 1e-6).  bench.py's N>1
+path uses the same split with RCCL over xGMI; on the 8-GPU node it is the
+driver that runs it."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from helpers import flat_from_export, oracle_cfg
+
+pytestmark = pytest.mark.gpu
+
+WORKER = r"""
+import os, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+import torch
+import torch.distributed as dist
+import pathtracerap_amd as P
+from pathtracerap_amd import synthetic
+from pathtracerap_amd.dist import render_sharded
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo")
+torch.cuda.set_device(0)
+s = P.Scene(synthetic.diffuse_scene({scene_dir!r}, ntri=3000, seed=31, metallic=True))
+s.build()
+cfg = P.RenderConfig(width=96, height=72, iterations={iters}, max_bounces=8)
+img = render_sharded(s, cfg, {iters})
+assert img.is_cuda
+if rank == 0:
+    np.save({out!r}, img.cpu().numpy())
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_render_sharded_hip_two_ranks(gpu, pt_mod, oracle_mod, tmp_path):
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    iters = 7                                         # odd: the ranks get 4 and 3 iterations
+    scene_dir = str(tmp_path / "scene")
+    out = str(tmp_path / "img.npy")
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT, scene_dir=scene_dir, iters=iters, out=out))
+    synthetic.diffuse_scene(scene_dir, ntri=3000, seed=31, metallic=True)   # both ranks read it
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=240)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    got = np.load(out).reshape(-1, 3)
+
+    s = P.Scene(synthetic.diffuse_scene(scene_dir, ntri=3000, seed=31, metallic=True))
+    s.build()
+    cfg = P.RenderConfig(width=96, height=72, iterations=iters, max_bounces=8)
+    r = P.Renderer(cfg)
+    r.allocateOnGPU(s)
+    r.renderLoop()
+    single = r.image()
+    r.free()
+    want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg, threads=16))
+    assert np.array_equal(single.view(np.uint32), want.view(np.uint32))
+    assert np.abs(got).sum() > 0
+    np.testing.assert_allclose(got, single, rtol=1e-6, atol=1e-6)
