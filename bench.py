@@ -202,7 +202,7 @@ def timed_run(P, ctx, scene, cfg, K, W, iter_base, events, reduce_image):
     pb0 = r.segments_per_bounce()
     if events:
         r.kernel_stats()                   # reset
-        r.set_profiling(True)
+        r.set_profiling(2)                 # event pairs around pipeline 0's trace phases only
     ctx.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -358,45 +358,51 @@ def main():
         r_main = rates(main_res, K, npix, world)
         roof = None
         stats = main_res["stats"]
-        split = bool(stats and stats.get("trace_launches", 0) > 0)
-        if stats and split:
-            # Dominant kernel: the persistent trace of bounces >= 1 (k_trace_gf / k_trace_bvh; one
-            # "launch" = one bounce's trace phase: main launch + tail launches + k_trace_deferred,
-            # bracketed by one event pair on the pipeline's stream).  Algorithmic bytes per
-            # segment entering bounce b >= 1: 32 B ray read (o, d) + 20 B hit record write.
+        if stats and stats.get("trace_launches", 0) > 0:
+            # Dominant kernel: the persistent trace of bounces >= 1 (k_trace_gf / k_trace_bvh).
+            # Algorithmic bytes per segment entering bounce b >= 1: 32 B ray read (o, d) + 20 B
+            # hit record write.  `achieved` = those bytes per step / ms_per_step: the launches of
+            # the 16 iterations in flight overlap, so the step's wall time is the time the
+            # kernel's work takes (a slight under-estimate: the other kernels share that time).
             kname = "k_trace_bvh" if args.accel == "bvh" else "k_trace_gf"
             tb_step = trace_bytes_per_step(per_bounce, K)
-            launches = max(stats["trace_launches"], 1)
-            nbytes = tb_step * K / launches              # per launch (this rank)
+            phases = max(1, len(per_bounce) - 1)                 # trace phases per step
+            job = tb_step / (main_res["elapsed"] / K) / 1e9      # per GPU: each rank runs K steps
+            # one "launch" = one bounce's trace phase (main launch + tail launches +
+            # k_trace_deferred), timed by an event pair on pipeline 0's stream in the timed region
+            launches = stats["trace_launches"]
             kms = stats["trace_ms"] / launches
-            achieved = nbytes / (kms / 1e3) / 1e9
-            job = tb_step / (main_res["elapsed"] / K) / 1e9     # per GPU: each rank runs K steps
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": load_pmc(kname, workload_key),
-                    "kernel": kname, "algorithmic_bytes_per_launch": round(nbytes), "avg_launch_ms": round(kms, 4),
-                    "launches": launches, "pipelines": main_res["pipes"],
-                    "measured": "HIP events around every trace phase inside the timed region, on the "
-                                "pipeline streams (launches of different iterations overlap)",
-                    "whole_job": {"algorithmic_bytes_per_step": round(tb_step), "ms_per_step": r_main["ms_per_step"],
-                                  "achieved": round(job, 2), "frac": round(job / HBM_PEAK_GBS, 5),
-                                  "why_launches_exceed_step": (
-                                      f"{launches / K:.0f} trace phases per step x {kms:.3f} ms = "
-                                      f"{launches / K * kms:.2f} ms of launch time per step against "
-                                      f"{r_main['ms_per_step']:.3f} ms per step: {main_res['pipes']} iterations "
-                                      f"are in flight, so about {launches / K * kms / r_main['ms_per_step']:.1f} "
-                                      f"trace phases run at once")},
-                    "sort_avg_ms": round(stats["sort_ms"] / max(stats["sort_launches"], 1), 4),
-                    "shade_avg_ms": round(stats["bounce_ms"] / max(stats["bounce_launches"], 1), 4),
-                    "first_bounce_avg_ms": round(stats["first_ms"] / max(stats["first_launches"], 1), 4),
-                    "scan_avg_ms": round(stats["scan_ms"] / max(stats["scan_launches"], 1), 4)}
+            b_launch = tb_step / phases
+            a_launch = b_launch / (kms / 1e3) / 1e9
+            tr = load_pmc(kname, workload_key)                   # HBM bytes per launch, one pipeline
+            roof = {"bound": "hbm", "achieved": round(job, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(job / HBM_PEAK_GBS, 5),
+                    "traffic": None if tr is None else round(tr * phases),
+                    "kernel": kname, "basis": "per step: algorithmic trace bytes per step / ms_per_step "
+                                              "(traffic: PMC HBM bytes per launch x trace phases per step)",
+                    "algorithmic_bytes_per_step": round(tb_step), "ms_per_step": r_main["ms_per_step"],
+                    "trace_phases_per_step": phases, "traffic_per_launch": None if tr is None else round(tr),
+                    "per_launch": {
+                        "avg_launch_ms": round(kms, 4), "algorithmic_bytes_per_launch": round(b_launch),
+                        "achieved": round(a_launch, 2), "frac": round(a_launch / HBM_PEAK_GBS, 5),
+                        "launches_timed": launches, "pipelines": main_res["pipes"],
+                        "measured": "HIP event pair around each of pipeline 0's trace phases inside the timed region",
+                        "why_launches_exceed_step": (
+                            f"{phases} trace phases per step x {kms:.3f} ms = {phases * kms:.2f} ms of launch "
+                            f"time per step against {r_main['ms_per_step']:.3f} ms per step: "
+                            f"{main_res['pipes']} iterations are in flight, so about "
+                            f"{phases * kms / r_main['ms_per_step']:.1f} trace phases run at once")}}
             if stats1 and stats1.get("trace_launches", 0) > 0:
                 l1 = stats1["trace_launches"]
                 k1 = stats1["trace_ms"] / l1
-                a1 = tb_step * K / l1 / (k1 / 1e3) / 1e9
+                a1 = b_launch / (k1 / 1e3) / 1e9
                 roof["single_pipeline"] = {"avg_launch_ms": round(k1, 4), "achieved": round(a1, 2),
                                            "frac": round(a1 / HBM_PEAK_GBS, 5), "launches": l1,
                                            "sort_avg_ms": round(stats1["sort_ms"] / max(stats1["sort_launches"], 1), 4),
-                                           "shade_avg_ms": round(stats1["bounce_ms"] / max(stats1["bounce_launches"], 1), 4)}
+                                           "shade_avg_ms": round(stats1["bounce_ms"] / max(stats1["bounce_launches"], 1), 4),
+                                           "scan_avg_ms": round(stats1["scan_ms"] / max(stats1["scan_launches"], 1), 4),
+                                           "measured": "HIP events, a separate pass of the same iterations with one "
+                                                       "pipeline (no overlap), rank 0"}
         # Issue roofline: the traces are bound by instruction issue and dependent-load
         # latency, not by HBM bytes, so the VALU issue rate against the SIMDs' peak is
         # the informative fraction -- for the whole job (all kernels of a step, with the

@@ -133,6 +133,8 @@ long long pt_renderer_segments(pt_renderer *r);
 long long pt_renderer_trace_faults(pt_renderer *r);
 /* out[b] = live rays entering bounce b, summed over the iterations rendered (b < n, n <= 64 useful). */
 int pt_renderer_segments_per_bounce(pt_renderer *r, long long *out, int n);
+/* HIP-event timing read by kernel_stats: 0 off, 1 around every kernel group on every
+ * pipeline, 2 around pipeline 0's trace phases only (light enough for a timed run). */
 int pt_renderer_set_profiling(pt_renderer *r, int on);
 /* Iterations in flight after allocate_on_gpu (config.pipelines clamped to 1..16, PT_PIPES overrides). */
 int pt_renderer_pipelines(pt_renderer *r);

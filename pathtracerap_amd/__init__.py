@@ -342,8 +342,9 @@ class Renderer:
         """Iterations in flight (own HIP streams) once allocated."""
         return _err(lib().pt_renderer_pipelines(self._h), "pipelines")
 
-    def set_profiling(self, on: bool) -> None:
-        _err(lib().pt_renderer_set_profiling(self._h, 1 if on else 0), "set_profiling")
+    def set_profiling(self, on) -> None:
+        """HIP-event timing: False/0 off, True/1 every kernel group, 2 pipeline 0's trace phases only."""
+        _err(lib().pt_renderer_set_profiling(self._h, int(on)), "set_profiling")
 
     def kernel_stats(self) -> dict:
         st = (ctypes.c_double * 11)()

@@ -250,7 +250,7 @@ int pt_renderer_pipelines(pt_renderer* r) {
     if (!r || !r->r) return set_err("null renderer");
     return r->r->pipelines();
 }
-int pt_renderer_set_profiling(pt_renderer* r, int on) { R_CALL(r->r->setProfiling(on != 0)); }
+int pt_renderer_set_profiling(pt_renderer* r, int on) { R_CALL(r->r->setProfiling(on)); }
 int pt_renderer_kernel_stats(pt_renderer* r, double st[7]) {
     if (!r || !r->r || !st) return set_err("null argument");
     pt::KernelStats k;

@@ -78,6 +78,8 @@ struct KParams {
     int* sort_bins;                     // [kSortBins] rays per key, [kSortBins] scatter cursors; zeroed by k_scan
     unsigned short* sort_key;           // per source index of the previous bounce's pool
     int sort_mode;                      // key layout (k_sort_hist); 0 = no sort
+    int hit_order;                      // 1: hit records at claim positions, slot_pos[j] = j's position (PT_HIT_ORDER)
+    int* slot_pos;
     float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
@@ -92,6 +94,8 @@ struct KParams {
                                         // hands nothing on.  Record buffers alternate between levels
     int drain_dump;                     // hand a wave's rays on once the pool is exhausted and <= this many
                                         // lanes still trace (0: off; PT_DRAIN_DUMP overrides)
+    const float4* top_nodes;            // k_trace_gf (PT_GF_TOP > 0): the top BLAS levels of mesh top_mesh, BFS
+    int top_mesh;                       // order, staged in LDS (inner links into the table carry kTopFlag)
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,
                                         // counted in segments[kTraceFaultCounter]); PT_TRACE_ITER_CAP overrides
 };
@@ -128,7 +132,7 @@ public:
 
     int setStream(hipStream_t s);
     int bindImage(float* device_rgb);
-    int setProfiling(bool on);
+    int setProfiling(int on);              // 0 off, 1 every kernel group, 2 pipeline 0's trace phases
     int kernelStats(KernelStats* out);
     long long segments();
     long long traceFaults();                         // waves that gave up (see kTraceFaultCounter); -1 on error
@@ -168,7 +172,7 @@ private:
     bool cache_valid = false;        // is_first_intersection_cached (Renderer.cpp:580)
     bool external_image = false;
     float* ext_image = nullptr;
-    bool profiling = false;
+    int profiling = 0;
     std::vector<void*> allocs;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> bounce_events, first_events, scan_events, trace_events, sort_events;
     bool split_trace = false;        // persistent k_trace_bvh / k_trace_gf + shading pass

@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     j = base + __popcll(idle & ((1ull << lane) - 1ull));
                     if (j < n) {
                         int src;
-                        if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
+                        if (p.order) { const int2 e = p.order[j]; j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
                         else src = slot_source(p, j);
                         const float4 a = p.ray[in_buf][0][src];
                         const float4 b = p.ray[in_buf][1][src];
@@ -1618,6 +1618,16 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
+// LDS staging of the top BLAS levels (north_star: "BVH nodes ... staged in LDS").
+// PT_GF_TOP nodes (whole levels: 1, 3, 7 or 15) of one mesh's binary BLAS -- the
+// mesh with the most triangles -- are copied to LDS at kernel start; a node
+// index with kTopFlag set is a slot of that table.  0: off.
+#ifndef PT_GF_TOP
+#define PT_GF_TOP 0
+#endif
+constexpr int kGfTop = PT_GF_TOP;
+constexpr int kTopFlag = 0x40000000;
+static_assert(kGfTop == 0 || kGfTop == 1 || kGfTop == 3 || kGfTop == 7 || kGfTop == 15, "PT_GF_TOP: whole levels");
 
 // Collection window of k_trace_gf, on voxel boxes instead of the reach R: the
 // walk can enter member h's voxel box before X = t_min + window only if the
@@ -1664,6 +1674,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
     __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
+    __shared__ float4 s_top[kGfTop > 0 ? 4 * kGfTop : 1];
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
@@ -1689,6 +1700,12 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         __syncthreads();
     }
     const ModelRec* models = lds_models ? s_models : p.models;
+    if (kGfTop > 0) {
+        for (int i = threadIdx.x; i < 4 * kGfTop; i += BS) s_top[i] = p.top_nodes[i];
+        __syncthreads();
+    }
+    // the root of model M's collection: the LDS table's slot 0 for the staged mesh
+    auto root_of = [&](const ModelRec& M) { return (kGfTop > 0 && M.mesh == p.top_mesh) ? kTopFlag : M.bvh_root; };
     const int n = p.n_live[bounce];
     const int in_buf = (bounce + 1) & 1;
     const int lane = threadIdx.x & 63;
@@ -1801,7 +1818,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
                     int src;
-                    if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
+                    if (p.order) { const int2 e = p.order[j]; j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
                     else src = slot_source(p, j);
                     const float4 a = p.ray[in_buf][0][src];
                     const float4 b = p.ray[in_buf][1][src];
@@ -1885,7 +1902,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 if (PT_TRACE_STATS && (p.debug & 1024)) G = mk3(0, 0, 0);   // timing-only ablation: no growth
                 tier = 0;
                 win = (PT_TRACE_STATS && (p.debug & 256)) ? 0.0f : M.wdelta;   // 256: timing-only ablation
-                cur = M.bvh_root;
+                cur = root_of(M);
                 sp = 0; nh = 0; tmin = kFMax; pblk = -1;
                 state = 2;
                 break;
@@ -1978,10 +1995,29 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             }
         } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
             const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-            const float4 q0 = nodes[4 * cur + 0];
-            const float4 q1 = nodes[4 * cur + 1];
-            const float4 q2 = nodes[4 * cur + 2];
-            const float4 q3 = nodes[4 * cur + 3];
+            float4 q0, q1, q2, q3;
+            if (kGfTop > 0) {
+                // staged slot: an unconditional LDS read (clamped slot), the global node only for
+                // the lanes below the table (typed pointers keep the two loads apart)
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(3))) const v4f lds_v4;
+                typedef __attribute__((address_space(1))) const v4f glb_v4;
+                const bool top = (cur & kTopFlag) != 0;
+                const int ti = top ? min(cur & 15, kGfTop - 1) : 0;
+                const lds_v4* t = (const lds_v4*)(s_top + 4 * ti);
+                v4f a0 = t[0], a1 = t[1], a2 = t[2], a3 = t[3];
+                if (!top) {
+                    const glb_v4* g = (const glb_v4*)(nodes + 4 * (size_t)cur);
+                    a0 = g[0]; a1 = g[1]; a2 = g[2]; a3 = g[3];
+                }
+                q0 = make_float4(a0.x, a0.y, a0.z, a0.w); q1 = make_float4(a1.x, a1.y, a1.z, a1.w);
+                q2 = make_float4(a2.x, a2.y, a2.z, a2.w); q3 = make_float4(a3.x, a3.y, a3.z, a3.w);
+            } else {
+                q0 = nodes[4 * cur + 0];
+                q1 = nodes[4 * cur + 1];
+                q2 = nodes[4 * cur + 2];
+                q3 = nodes[4 * cur + 3];
+            }
             const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
             const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
             const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
@@ -2030,7 +2066,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 const ModelRec& M = models[im];
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = M.bvh_root;
+                cur = root_of(M);
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2068,7 +2104,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             } else {                                    // not provably exact: next tier's collection
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = M.bvh_root;
+                cur = root_of(M);
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2152,8 +2188,8 @@ __global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt > 0)      // every build: which route the rays took
         atomicAdd(p.segments + kDeferredRayCounter, (unsigned long long)cnt);
     for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
-        const int j = p.defer_slots[q];
-        const int src = slot_source(p, j);
+        const int j = p.defer_slots[q];              // hit_order: the claim position
+        const int src = p.hit_order ? p.order[j].y : slot_source(p, j);
         const float4 a = p.ray[in_buf][0][src];
         const float4 b = p.ray[in_buf][1][src];
         const Hit h = intersect_scene<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
@@ -2218,11 +2254,12 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
             r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
             r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
             r.c = mk3(c.x, c.y, c.z);
-            if (ACCEL == kAccelHitBuffer) {       // traced by k_trace_bvh
-                const float4 hh = p.hit4[j];
+            if (ACCEL == kAccelHitBuffer) {       // traced by k_trace_bvh / k_trace_gf
+                const int hj = p.hit_order ? p.slot_pos[j] : j;   // hit_order: records sit in claim order
+                const float4 hh = p.hit4[hj];
                 h.dist = hh.x;
                 h.n = mk3(hh.y, hh.z, hh.w);
-                h.model = p.hitm[j];
+                h.model = p.hitm[hj];
             } else {
                 h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
             }
@@ -2494,7 +2531,11 @@ __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce)
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < kSortPer; t++)
-        if (key[t] >= 0) p.order[s_h[key[t]] + rank[t]] = make_int2(jj[t], i0 + t * kSortWG + tid);
+        if (key[t] >= 0) {
+            const int pos = s_h[key[t]] + rank[t];
+            p.order[pos] = make_int2(jj[t], i0 + t * kSortWG + tid);
+            if (p.hit_order) p.slot_pos[jj[t]] = pos;
+        }
 }
 
 __global__ void k_selftest_math(int n, const float* x, const float* y, float* out) {
@@ -2699,6 +2740,11 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         // auto: key 7 for both persistent traces (bvh: 3421 -> 3571 Mrays/s at 8 waves per CU, 16 pipelines)
         const int want = so ? std::atoi(so) : cfg.ray_sort >= 0 ? cfg.ray_sort : 7;
         kp.sort_mode = (split_trace && !block_claims) ? std::max(0, std::min(8, want)) : 0;
+        // PT_HIT_ORDER=1: the traces write hit records at the ray's claim position (rays claimed
+        // together finish close in time, so their records share L2 lines before write-back); the
+        // shading pass finds slot j's record through slot_pos[j].  Results identical.
+        const char* ho = std::getenv("PT_HIT_ORDER");
+        kp.hit_order = kp.sort_mode && ho && std::atoi(ho) != 0;
         float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
         for (const ModelRec& m : scene.model_recs)
             for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], m.wbox[a]); hi[a] = std::max(hi[a], m.wbox[3 + a]); }
@@ -2709,6 +2755,32 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         }
     }
     kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr;
+    kp.top_nodes = nullptr;
+    kp.top_mesh = -1;
+    if (kGfTop > 0 && cfg.accel == ACCEL_GRID_FAST) {
+        // k_trace_gf's LDS table: the first kGfTop nodes, breadth first, of the BLAS of the
+        // mesh with the most triangles; inner links into the table become kTopFlag | slot
+        long long most = -1;
+        for (const ModelRec& m : scene.model_recs)
+            if ((long long)m.tri_end - m.tri_start > most) { most = (long long)m.tri_end - m.tri_start; kp.top_mesh = m.mesh; }
+        std::vector<BvhNode> top(kGfTop);
+        std::memset(top.data(), 0, top.size() * sizeof(BvhNode));
+        std::vector<int> gid{scene.mesh_bvh_root[kp.top_mesh]};
+        for (size_t i = 0; i < gid.size(); i++) {
+            const BvhNode& nd = scene.bvh_nodes[gid[i]];
+            if (nd.count0 == 0 && (int)gid.size() < kGfTop) gid.push_back(nd.link0);
+            if (nd.count1 == 0 && (int)gid.size() < kGfTop) gid.push_back(nd.link1);
+        }
+        for (size_t i = 0; i < gid.size(); i++) {
+            BvhNode nd = scene.bvh_nodes[gid[i]];
+            for (size_t k = 1; k < gid.size(); k++) {
+                if (nd.count0 == 0 && nd.link0 == gid[k]) nd.link0 = kTopFlag | (int)k;
+                if (nd.count1 == 0 && nd.link1 == gid[k]) nd.link1 = kTopFlag | (int)k;
+            }
+            top[i] = nd;
+        }
+        PT_HIP(upload(allocs, &kp.top_nodes, top.data(), top.size() * sizeof(BvhNode), stream));
+    }
     PT_HIP(upload(allocs, &kp.segments, nullptr, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.segments, 0, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     // Pipelines: iterations in flight on their own streams, each with its own
@@ -2769,6 +2841,7 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
         PT_HIP(upload(allocs, &k.order, nullptr, cap * sizeof(int2), st));
         PT_HIP(upload(allocs, &k.sort_key, nullptr, cap * sizeof(unsigned short), st));
         PT_HIP(upload(allocs, &k.sort_bins, nullptr, 2 * kSortBins * sizeof(int), st));
+        PT_HIP(upload(allocs, &k.slot_pos, nullptr, (k.hit_order ? cap : 1) * sizeof(int), st));
         PT_HIP(hipMemsetAsync(k.sort_bins, 0, 2 * kSortBins * sizeof(int), st));
     }
     const size_t hcap = split_trace ? cap : 1;
@@ -2905,45 +2978,49 @@ void Renderer::launchBounce(const KParams& k, hipStream_t st, bool first, dim3 g
 int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
     const KParams& k = pk[q];
     const dim3 grid((unsigned)kp.nblocks + 8u);
+    // profiling 1: an event pair around every kernel group on every pipeline; 2: around the
+    // trace phases of pipeline 0 only (cheap enough for a timed region: 1/16 of the pairs)
+    const bool pall = profiling == 1, ptrace = pall || (profiling == 2 && q == 0);
     for (int b = 0; b < passes; b++) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (b > 0 && split_trace) {
             if (k.order) {
-                if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+                if (pall) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
                 const dim3 sg((unsigned)((k.nblocks * (size_t)k.chunk + kSortWG * kSortPer - 1) / (kSortWG * kSortPer)));
                 hipLaunchKernelGGL(k_sort_hist, sg, dim3(kSortWG), 0, st, k, b);
                 hipLaunchKernelGGL(k_sort_prefix, dim3(1), dim3(kSortWG), 0, st, k);
                 hipLaunchKernelGGL(k_sort_scatter, sg, dim3(kSortWG), 0, st, k, b);
-                if (profiling) { hipEventRecord(e1, st); sort_events.push_back({e0, e1}); e0 = e1 = nullptr; }
+                if (pall) { hipEventRecord(e1, st); sort_events.push_back({e0, e1}); e0 = e1 = nullptr; }
             }
             // the trace pair brackets the trace launches only (not the sort kernels)
-            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+            if (ptrace) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             launchTrace(k, st, b);
             PT_HIP(hipGetLastError());
-            if (profiling) {
+            if (ptrace) {
                 hipEventRecord(e1, st);
                 trace_events.push_back({e0, e1});
-                hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st);
+                e0 = e1 = nullptr;
             }
+            if (pall) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             launchBounce(k, st, false, grid, iter, b, kAccelHitBuffer);
         } else {
-            if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+            if (pall) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
             launchBounce(k, st, b == 0, grid, iter, b, cfg.accel);
         }
         PT_HIP(hipGetLastError());
-        if (profiling) {
+        if (pall) {
             hipEventRecord(e1, st);
             (b == 0 ? first_events : bounce_events).push_back({e0, e1});
             e0 = e1 = nullptr;
         }
-        if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
+        if (pall) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanWG), 0, st, k, b);
         PT_HIP(hipGetLastError());
         if (k.use_slotmap && b + 1 < passes) {
             hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((k.nblocks * k.chunk + 255) / 256)), dim3(256), 0, st, k, b);
             PT_HIP(hipGetLastError());
         }
-        if (profiling) { hipEventRecord(e1, st); scan_events.push_back({e0, e1}); }
+        if (pall) { hipEventRecord(e1, st); scan_events.push_back({e0, e1}); }
     }
     return 0;
 }
@@ -2962,9 +3039,9 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
     if (!kp.image || !kp.cache_hit || !kp.models) { last_error = "renderLoop: device buffers missing"; return -1; }
     if (!cache_valid) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (profiling) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
+        if (profiling == 1) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, stream); }
         if (launchPrimary() != 0) return -1;
-        if (profiling) {
+        if (profiling == 1) {
             hipEventRecord(e1, stream);
             hipEventSynchronize(e1);
             float ms = 0;
@@ -3069,7 +3146,8 @@ int Renderer::checkFaults() {
     return 0;
 }
 
-int Renderer::setProfiling(bool on) {
+int Renderer::setProfiling(int on) {
+    if (on < 0 || on > 2) { last_error = "profiling level must be 0, 1 or 2"; return -1; }
     profiling = on;
     return 0;
 }

@@ -94,7 +94,7 @@ def write_obj(path: str, pos, nrm, tris) -> None:
 
 
 def diffuse_scene(out_dir: str, ntri: int = 100_000, seed: int = 0, width: int = 1280, height: int = 1024,
-                  iterations: int = 256, bounces: int = 8, accel: str = "bvh", metallic: bool = False) -> str:
+                  iterations: int = 256, bounces: int = 8, accel: str = "grid_fast", metallic: bool = False) -> str:
     """Writes the OBJs and a Config.txt-grammar scene file; returns its path.
 
     configs[1]: diffuse-only OBJ (~100k tris), 1280x1024, 256 spp, 8 bounces.

@@ -499,3 +499,22 @@ def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypat
     img, seg, oimg, oseg = _render_both(P, O, s, cfg)
     assert seg == oseg
     assert_bitexact(img, oimg, f"PT_WALK_HANDON={handon} PT_WALK_WCAP={wcap} pipes={pipes} {scene}")
+
+
+@pytest.mark.parametrize("accel", [1, 2])
+@pytest.mark.parametrize("pipes", [1, 4])
+def test_hit_order_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, pipes):
+    """PT_HIT_ORDER=1: the persistent traces write hit records at the rays' claim
+    positions of the ray sort and the shading pass finds them through slot_pos;
+    deferred rays, drain continuations and walk hand-ons carry the position.
+    Images and segment counts stay the oracle's."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_HIT_ORDER", "1")
+    for path in (synthetic.diffuse_scene(synth_dir, ntri=6000, seed=17, metallic=True), REF_SCENE):
+        s = P.Scene(path)
+        s.build()
+        cfg = P.RenderConfig(width=157, height=83, iterations=3, max_bounces=7, accel=accel, pipelines=pipes)
+        img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+        assert seg == oseg
+        assert_bitexact(img, oimg, f"PT_HIT_ORDER accel={accel} pipes={pipes}")
