@@ -12,7 +12,7 @@
 #   pmc[=ARGS]            FETCH_SIZE and WRITE_SIZE, one --pmc pass each, of bench.py ARGS
 #   counters=C1,C2@ARGS   one --pmc pass of the listed counters (within one pass's limits)
 #   ab=ARGS               python scripts/ab.py ARGS (interleaved in-process A/B)
-#   ablib=R:SPEC:N1,N2    R interleaved rounds of ab.py SPEC over library builds
+#   ablib=R@SPEC@N1,N2    R interleaved rounds of ab.py SPEC over library builds
 #                         (build_variants/lib_N.so from scripts/build_variant.sh; "default" = in-tree)
 #   py=SCRIPT ARGS        python SCRIPT ARGS (a measurement script under scripts/)
 #
@@ -67,7 +67,7 @@ for step in "$@"; do
       timeout -k 10 900 python -u scripts/ab.py $arg > gpurun_out/$tag.json 2> gpurun_out/$tag.err
       rc=$?; cat gpurun_out/$tag.json; tail -3 gpurun_out/$tag.err ;;
     ablib)
-      IFS=: read -r rounds spec names <<< "$arg"
+      IFS=@ read -r rounds spec names <<< "$arg"
       rc=0
       for r in $(seq 1 "$rounds"); do
         for lib in ${names//,/ }; do
