@@ -386,7 +386,10 @@ def main():
                         "avg_launch_ms": round(kms, 4), "algorithmic_bytes_per_launch": round(b_launch),
                         "achieved": round(a_launch, 2), "frac": round(a_launch / HBM_PEAK_GBS, 5),
                         "launches_timed": launches, "pipelines": main_res["pipes"],
-                        "measured": "HIP event pair around each of pipeline 0's trace phases inside the timed region",
+                        "measured": "HIP event pair around each of pipeline 0's trace phases inside the timed "
+                                    "region: from the phase's turn on its stream to its last launch's end, so it "
+                                    "includes waiting for CU slots the other pipelines' kernels hold (rocprofv3 "
+                                    "times execution only: profiles/r03/kernel_stats_grid_fast_16p.csv)",
                         "why_launches_exceed_step": (
                             f"{phases} trace phases per step x {kms:.3f} ms = {phases * kms:.2f} ms of launch "
                             f"time per step against {r_main['ms_per_step']:.3f} ms per step: "

@@ -93,6 +93,12 @@ def write_obj(path: str, pos, nrm, tris) -> None:
                    fmt="f %d//%d %d//%d %d//%d")
 
 
+def _write_atomic(path, pos, nrm, tris):
+    tmp = f"{path}.{os.getpid()}.tmp"
+    write_obj(tmp, pos, nrm, tris)
+    os.replace(tmp, path)
+
+
 def diffuse_scene(out_dir: str, ntri: int = 100_000, seed: int = 0, width: int = 1280, height: int = 1024,
                   iterations: int = 256, bounces: int = 8, accel: str = "grid_fast", metallic: bool = False) -> str:
     """Writes the OBJs and a Config.txt-grammar scene file; returns its path.
@@ -104,11 +110,11 @@ def diffuse_scene(out_dir: str, ntri: int = 100_000, seed: int = 0, width: int =
     tag = f"torus_{ntri}_{seed}"
     obj = os.path.join(out_dir, tag + ".obj")
     if not os.path.exists(obj):
-        write_obj(obj, *torus_mesh(ntri, seed=seed))
+        _write_atomic(obj, *torus_mesh(ntri, seed=seed))
     for name, fn in (("room", room_mesh), ("light", light_mesh)):
         p = os.path.join(out_dir, name + ".obj")
         if not os.path.exists(p):
-            write_obj(p, *fn())
+            _write_atomic(p, *fn())
     lines = [
         "# synthetic scene (pathtracerap_amd.synthetic.diffuse_scene)",
         "", "RENDER", f"resolution:[{width},{height}]", f"iterations:{iterations}",
@@ -129,8 +135,10 @@ def diffuse_scene(out_dir: str, ntri: int = 100_000, seed: int = 0, width: int =
         "material:" + ("blue_coat" if metallic else "red"),
     ]
     path = os.path.join(out_dir, f"scene_{tag}{'_metal' if metallic else ''}.txt")
-    with open(path, "w") as f:
+    tmp = f"{path}.{os.getpid()}.tmp"          # atomic: another process may be reading the old file
+    with open(tmp, "w") as f:
         f.write("\n".join(lines) + "\n")
+    os.replace(tmp, path)
     return path
 
 

@@ -25,12 +25,11 @@ import numpy as np
 import torch
 import torch.distributed as dist
 import pathtracerap_amd as P
-from pathtracerap_amd import synthetic
 from pathtracerap_amd.dist import render_sharded
 rank = int(os.environ["RANK"])
 dist.init_process_group("gloo")
 torch.cuda.set_device(0)
-s = P.Scene(synthetic.diffuse_scene({scene_dir!r}, ntri=3000, seed=31, metallic=True))
+s = P.Scene({scene_path!r})          # written once by the parent
 s.build()
 cfg = P.RenderConfig(width=96, height=72, iterations={iters}, max_bounces=8)
 img = render_sharded(s, cfg, {iters})
@@ -57,8 +56,8 @@ def test_render_sharded_hip_two_ranks(gpu, pt_mod, oracle_mod, tmp_path):
     scene_dir = str(tmp_path / "scene")
     out = str(tmp_path / "img.npy")
     script = tmp_path / "worker.py"
-    script.write_text(WORKER.format(root=ROOT, scene_dir=scene_dir, iters=iters, out=out))
-    synthetic.diffuse_scene(scene_dir, ntri=3000, seed=31, metallic=True)   # both ranks read it
+    scene_path = synthetic.diffuse_scene(scene_dir, ntri=3000, seed=31, metallic=True)   # both ranks read it
+    script.write_text(WORKER.format(root=ROOT, scene_path=scene_path, iters=iters, out=out))
     port = _free_port()
     procs = []
     for rank in range(2):
@@ -77,7 +76,7 @@ def test_render_sharded_hip_two_ranks(gpu, pt_mod, oracle_mod, tmp_path):
     assert all(p.returncode == 0 for p in procs), "\n".join(logs)
     got = np.load(out).reshape(-1, 3)
 
-    s = P.Scene(synthetic.diffuse_scene(scene_dir, ntri=3000, seed=31, metallic=True))
+    s = P.Scene(scene_path)
     s.build()
     cfg = P.RenderConfig(width=96, height=72, iterations=iters, max_bounces=8)
     r = P.Renderer(cfg)
