@@ -62,7 +62,10 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
-constexpr int kSortBits = 12, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
+#ifndef PT_SORT_BITS
+#define PT_SORT_BITS 12       // ray sort key bits (14: key 9, 15: key 10 -- finer cells, bigger LDS histograms)
+#endif
+constexpr int kSortBits = PT_SORT_BITS, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
 #ifndef PT_SORT_WG
 #define PT_SORT_WG 512
 #endif
@@ -2439,6 +2442,21 @@ __device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
                    (((a >> 2) & 1) << 5) | (((b >> 2) & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) |
                    ((a & 1) << 1) | (b & 1);
         }
+        case 9: { // 14 bits, interleaved, origin 4^3 and direction 16 x 16: u3 v3 x1 y1 z1 u2 v2 x0 y0 z0 u1 v1 u0 v0
+            const int a = iu >> 2, b = iv >> 2, x = ix >> 2, y = iy >> 2, z = iz >> 2;
+            return (((a >> 3) & 1) << 13) | (((b >> 3) & 1) << 12) | (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) |
+                   (((z >> 1) & 1) << 9) | (((a >> 2) & 1) << 8) | (((b >> 2) & 1) << 7) | ((x & 1) << 6) |
+                   ((y & 1) << 5) | ((z & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) |
+                   ((a & 1) << 1) | (b & 1);
+        }
+        case 10: { // 15 bits, interleaved, origin 8^3 and direction 8 x 8: x2 y2 z2 u2 v2 x1 y1 z1 u1 v1 x0 y0 z0 u0 v0
+            const int a = iu >> 3, b = iv >> 3, x = ix >> 1, y = iy >> 1, z = iz >> 1;
+            int m = 0;
+            for (int q = 2; q >= 0; q--)
+                m = (m << 5) | (((x >> q) & 1) << 4) | (((y >> q) & 1) << 3) | (((z >> q) & 1) << 2) |
+                    (((a >> q) & 1) << 1) | ((b >> q) & 1);
+            return m;
+        }
         default: { // interleaved: u2 v2 x1 y1 z1 u1 v1 x0 y0 z0 u0 v0 (u, v: 3 bits, x, y, z: 2 bits)
             const int a = iu >> 3, b = iv >> 3, x = ix >> 2, y = iy >> 2, z = iz >> 2;
             return (((a >> 2) & 1) << 11) | (((b >> 2) & 1) << 10) | (((x >> 1) & 1) << 9) | (((y >> 1) & 1) << 8) |
@@ -2739,7 +2757,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const bool block_claims = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & 4) : (kp.trace_flags & 4);
         // auto: key 7 for both persistent traces (bvh: 3421 -> 3571 Mrays/s at 8 waves per CU, 16 pipelines)
         const int want = so ? std::atoi(so) : cfg.ray_sort >= 0 ? cfg.ray_sort : 7;
-        kp.sort_mode = (split_trace && !block_claims) ? std::max(0, std::min(8, want)) : 0;
+        // keys 9 (14 bits) and 10 (15 bits) need a PT_SORT_BITS build that wide
+        const int max_key = kSortBits >= 15 ? 10 : kSortBits >= 14 ? 9 : 8;
+        kp.sort_mode = (split_trace && !block_claims) ? std::max(0, std::min(max_key, want)) : 0;
         // PT_HIT_ORDER=1: the traces write hit records at the ray's claim position (rays claimed
         // together finish close in time, so their records share L2 lines before write-back); the
         // shading pass finds slot j's record through slot_pos[j].  Results identical.
