@@ -23,20 +23,19 @@ enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2,
 //              ACCEL_GRID; needs the BVH.
 enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1, ACCEL_GRID_FAST = 2 };
 
-// One instance (Model, Primitive.h:237-244) flattened for the kernels.
-// 66 dwords; read with wave-uniform (scalar) loads inside the model loop.
+// One instance (Model, Primitive.h:237-244) flattened for the traces: 62
+// dwords (the material, which only the shading pass reads, is ModelShade), so
+// k_trace_gf stages up to 12 of them in LDS at 16 resident waves per CU.
 struct ModelRec {
     float w2m[12];        // world_to_model columns 0..3, rows 0..2 (m[c*3+k])
     float m2w[12];        // model_to_world, same packing
     float nm[9];          // inverse(mat3(model_to_world)): nm[r*3+c] = Inverse[r][c]
-    int mat_type;         // Material::MaterialType
     float bbox[6];        // mesh bounding box (model space) min3 max3
     float vw[3];          // grid voxel widths
     int vox_start;        // grid->voxelIndices.start_index
     int mesh;
     int tri_start, tri_end;
     int bvh_root;         // index of the mesh's BLAS root node
-    float color[3];       // Material::color
     float wbox[6];        // conservative world-space AABB of everything the instance can hit
     float reach;          // R: max over triangles of the (tolerance-grown) voxel-box diameter, model units
     int bvh4_root;        // index of the mesh's 4-wide BLAS root node
@@ -44,7 +43,13 @@ struct ModelRec {
     float ivw[3];         // 1 / vw (rounded; walk certificate only, used with margins)
     float cslack[3];      // walk certificate: position slack per axis (DDA +EPSILON shift + rounding)
 };
-static_assert(sizeof(ModelRec) == 66 * 4, "ModelRec layout");
+static_assert(sizeof(ModelRec) == 62 * 4, "ModelRec layout");
+
+// The instance's material (Primitive.h:211-227), read by the shading pass.
+struct ModelShade {
+    float color[3];       // Material::color
+    int mat_type;         // Material::MaterialType
+};
 
 // 2-wide BVH node: both children's boxes in one 64-byte line.
 // link/count: count == 0 -> link is a child node index; count > 0 -> link is

@@ -37,6 +37,7 @@ struct RenderConfig {            // Config.h + generateRaysKernel constants, at 
 struct KParams {
     // scene (read-only, stays L2/MALL resident)
     const ModelRec* models;
+    const ModelShade* shade;    // per model: material (shading pass)
     int nmodels;
     int gdim[3];
     const float4* tri_geom;     // 3 float4 per triangle: v0, e1, e2

@@ -1025,9 +1025,9 @@ __device__ __forceinline__ void shade(const KParams& p, RayState& r, const Hit& 
         const f3 dir = normalize(r.d);
         const f3 ip = r.o + dir * h.dist;
         if (r.bounces > 0) {
-            const ModelRec& M = p.models[h.model];
-            const int mt = M.mat_type;
-            const f3 mc = mk3(M.color[0], M.color[1], M.color[2]);
+            const ModelShade& S = p.shade[h.model];
+            const int mt = S.mat_type;
+            const f3 mc = mk3(S.color[0], S.color[1], S.color[2]);
             if (mt == MAT_DIFFUSE || mt == MAT_METAL || mt == MAT_COAT) {
                 Rng rng = Rng::make(iter, slot, r.bounces);
                 if (mt == MAT_DIFFUSE) r.d = scatter_hemisphere(h.n, rng);
@@ -1195,7 +1195,14 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 #ifndef PT_BVH_MINWAVES
 #define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
 #endif
-constexpr int kLdsModels = 8;    // model records staged in LDS when the scene has at most this many
+// Model records staged in LDS when the scene has at most this many: k_trace_gf
+// 12 (7168 B of lane state + 12 x 248 B = 10144 B per 64-lane workgroup, 16 per
+// CU), k_trace_bvh 8 (6144 + 8 x 248 = 8128 B, 20 per CU).
+#ifndef PT_LDS_MODELS_GF
+#define PT_LDS_MODELS_GF 12
+#endif
+constexpr int kLdsModels = 8;
+constexpr int kLdsModelsGf = PT_LDS_MODELS_GF;
 constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
 
 // Drain continuations.  Once a persistent trace's pool is exhausted its waves
@@ -1621,6 +1628,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
+#ifndef PT_CERT_CAP
+#define PT_CERT_CAP PT_GF_HITCAP   // members the main launch's walk certificate handles (walk hand-ons: the rest)
+#endif
+constexpr int kCertCap = PT_CERT_CAP;
 // LDS staging of the top BLAS levels (north_star: "BVH nodes ... staged in LDS").
 // PT_GF_TOP nodes (whole levels: 1, 3, 7 or 15) of one mesh's binary BLAS -- the
 // mesh with the most triangles -- are copied to LDS at kernel start; a node
@@ -1676,7 +1687,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     static_assert(kCX + 9 + kGfStack + 4 * kGfHitCap <= kContFields, "continuation record too small");
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
-    __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
+    __shared__ ModelRec s_models[(F & 1) ? kLdsModelsGf : 1];
     __shared__ float4 s_top[kGfTop > 0 ? 4 * kGfTop : 1];
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
@@ -1691,14 +1702,14 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     const int nd = TAIL ? p.cont_count[level - 1] : 0;
     const int ncont = nd + (TAIL && level == 1 ? min(p.cont_count[kDrainLevels], p.cont_wcap) : 0);
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
-    // F & 1 is launched only when the scene has at most kLdsModels models: the
+    // F & 1 is launched only when the scene has at most kLdsModelsGf models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
     // never flat loads through a generic pointer.
     constexpr bool lds_models = (F & 1) != 0;
     if (lds_models) {
         const int* src = reinterpret_cast<const int*>(p.models);
         int* dst = reinterpret_cast<int*>(s_models);
-        const int nw = min(p.nmodels, kLdsModels) * (int)(sizeof(ModelRec) / 4);
+        const int nw = min(p.nmodels, kLdsModelsGf) * (int)(sizeof(ModelRec) / 4);
         for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
         __syncthreads();
     }
@@ -2074,6 +2085,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 state = 2;
             }
         } else if ((phase & 8) && state == 5) {          // the walk: certificate, else the exact walk
+            if (PT_TRACE_STATS && (p.debug & 2048))       // walks by hit-set size: 1, 2, 3, >= 4 (pool: >= 4)
+                atomicAdd(p.segments + 51 + (pblk >= 0 ? 3 : min(nh, 4) - 1) + kMaxBounceCounters, 1ull);
             const ModelRec& M = models[im];
             const f3 pt = o + d * t_box;
             const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -2085,10 +2098,20 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 // the certificate only; a ray it cannot decide is handed on to the tail launch
                 // (which walks it exactly) or, past the records' room, to k_trace_deferred
                 int tri = -1;
-                const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
-                const bool ok = pblk < 0
-                    ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
-                    : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
+                bool ok;
+                if (kCertCap < kGfHitCap) {
+                    // the main launch certifies hit sets of at most kCertCap members (97 % of the
+                    // walks at configs[1]: 18 % one member, 79 % two -- a slab's two faces in one
+                    // voxel); larger ones and pool hit sets go to the tail launch with the rest
+                    const bool small = pblk < 0 && nh <= kCertCap;
+                    ok = small && walk_certify<kCertCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; },
+                                                         nh, tmin, win, tri);
+                } else {
+                    const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
+                    ok = pblk < 0
+                        ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
+                        : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
+                }
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
                 if (!ok) state = 6;
             } else {
@@ -2662,6 +2685,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     kp.nmodels = (int)scene.model_recs.size();
     for (int k = 0; k < 3; k++) kp.gdim[k] = scene.grid_dim[k];
     PT_HIP(upload(allocs, &kp.models, scene.model_recs.data(), scene.model_recs.size() * sizeof(ModelRec), stream));
+    PT_HIP(upload(allocs, &kp.shade, scene.model_shade.data(), scene.model_shade.size() * sizeof(ModelShade), stream));
     PT_HIP(upload(allocs, &kp.tri_geom, scene.tri_geom.data(), scene.tri_geom.size() * sizeof(float), stream));
     PT_HIP(upload(allocs, &kp.tri_normal, scene.tri_normal.data(), scene.tri_normal.size() * sizeof(float), stream));
     std::vector<int2> vox(scene.voxels.size());
@@ -2708,7 +2732,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
         const char* gff = std::getenv("PT_GF_FLAGS");
         gf_flags = gff ? std::atoi(gff) : 9;
-        if (scene.model_recs.size() > (size_t)kLdsModels) gf_flags &= ~1;     // model records stay in global memory
+        if (scene.model_recs.size() > (size_t)kLdsModelsGf) gf_flags &= ~1;   // model records stay in global memory
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
@@ -2908,8 +2932,8 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
         // model records in LDS: the variant asks for them (gf_flags & 1, cleared by
-        // allocateOnGPU when the scene has more than kLdsModels models)
-        const bool lds = (gf_flags & 1) && k.nmodels <= kLdsModels;
+        // allocateOnGPU when the scene has more than kLdsModelsGf models)
+        const bool lds = (gf_flags & 1) && k.nmodels <= kLdsModelsGf;
         switch (gf_flags) {
             case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b, 0); break;
             case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b, 0); break;

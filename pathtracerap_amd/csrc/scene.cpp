@@ -580,6 +580,7 @@ void Scene::buildDeviceTables() {
         std::memcpy(&bvh_tri_geom[i * 12 + 11], &tri_vbox[2 * (size_t)t + 1], sizeof(int));
     }
     model_recs.resize(models.size());
+    model_shade.resize(models.size());
     for (size_t i = 0; i < models.size(); i++) {
         const Model& m = models[i];
         ModelRec& r = model_recs[i];
@@ -590,7 +591,6 @@ void Scene::buildDeviceTables() {
                 r.m2w[c * 3 + k] = m.model_to_world[c * 4 + k];
             }
         m3_inverse_of_m4(m.model_to_world, r.nm);
-        r.mat_type = m.mat.material_type;
         const Mesh& mesh = meshes[m.mesh_index];
         r.bbox[0] = mesh.bounding_box.min.x; r.bbox[1] = mesh.bounding_box.min.y; r.bbox[2] = mesh.bounding_box.min.z;
         r.bbox[3] = mesh.bounding_box.max.x; r.bbox[4] = mesh.bounding_box.max.y; r.bbox[5] = mesh.bounding_box.max.z;
@@ -603,7 +603,9 @@ void Scene::buildDeviceTables() {
         r.tri_end = mesh.triangle_indices.end_index;
         r.bvh_root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m.mesh_index];
         r.bvh4_root = mesh_bvh4_root.empty() ? -1 : mesh_bvh4_root[m.mesh_index];
-        for (int k = 0; k < 3; k++) r.color[k] = m.mat.color[k];
+        ModelShade& sh = model_shade[i];
+        for (int k = 0; k < 3; k++) sh.color[k] = m.mat.color[k];
+        sh.mat_type = m.mat.material_type;
         world_box(m, mesh, r.bvh_root, r.wbox);
         // Bounded hit-set collection (ACCEL_GRID_FAST).  A member h whose voxel box the
         // DDA enters at ray parameter tau has its hit within tau + R_h, R_h = the diameter

@@ -88,6 +88,7 @@ public:
     std::vector<float> tri_geom;      // 12 floats / triangle: v0.xyz,_, e1.xyz,_, e2.xyz,_
     std::vector<float> tri_normal;    // 4 floats / triangle: normalize((n0+n1+n2)*(1/3))
     std::vector<ModelRec> model_recs;
+    std::vector<ModelShade> model_shade;  // per model: material (shading pass)
     std::vector<BvhNode> bvh_nodes;   // all meshes' BLAS, concatenated
     std::vector<int> bvh_tri_order;   // leaf triangle references (global triangle index)
     std::vector<float> bvh_tri_geom;  // 12 floats / leaf reference: tri_geom in leaf order; w lanes carry
