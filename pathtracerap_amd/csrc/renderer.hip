@@ -203,6 +203,18 @@ __device__ bool grid_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3
 
 // Inverse direction for node tests: clamped to +-1e30 so the FMA form never
 // meets inf * 0 or inf - inf (a zero direction component stays a huge slope).
+// Slopes for the instance culling (model_culled): hardware reciprocals (v_rcp_f32,
+// 1 ulp) instead of correctly rounded divisions (about 10 instructions each).
+// The culling test only has to be conservative, and the world boxes it tests
+// are padded by 1e-4 of their diagonal + 0.01 (plus 1e-3 of the mesh diagonal
+// + 1 before the transform), far beyond a few ulps of the slab parameters.
+#ifndef PT_CULL_RCP
+#define PT_CULL_RCP 1
+#endif
+__device__ __forceinline__ f3 cull_inv(f3 d) {
+    if (PT_CULL_RCP) return mk3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    return mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+}
 __device__ __forceinline__ f3 node_inv(f3 inv) {
     return mk3(fminf(fmaxf(inv.x, -1e30f), 1e30f), fminf(fmaxf(inv.y, -1e30f), 1e30f), fminf(fmaxf(inv.z, -1e30f), 1e30f));
 }
@@ -985,7 +997,7 @@ template <int ACCEL, int STRIDE>
 __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs) {
     float gdist = kFMax;
     int gmodel = -1, gtri = -1;
-    const f3 winv = node_inv(mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z));
+    const f3 winv = node_inv(cull_inv(dir));
     const float dlen = sqrtf(dot(dir, dir));
     for (int im = 0; im < p.nmodels; im++) {
         const ModelRec& M = p.models[im];
@@ -1201,7 +1213,10 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 #ifndef PT_LDS_MODELS_GF
 #define PT_LDS_MODELS_GF 12
 #endif
-constexpr int kLdsModels = 8;
+#ifndef PT_LDS_MODELS_BVH
+#define PT_LDS_MODELS_BVH 8
+#endif
+constexpr int kLdsModels = PT_LDS_MODELS_BVH;
 constexpr int kLdsModelsGf = PT_LDS_MODELS_GF;
 constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
 
@@ -1305,7 +1320,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         best = __int_as_float(C[kCX * cs]); best_tri = C[(kCX + 1) * cs]; any = C[(kCX + 2) * cs] != 0;
 #pragma unroll 1
                         for (int q = 0; q < kStack; q++) stack[q * BS] = C[(kCX + 3 + q) * cs];
-                        winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                        winv = node_inv(cull_inv(dw));
                         dlen = sqrtf(dot(dw, dw));
                         if (state != 1) {                   // inside model im: its model-space ray, as selected
                             const ModelRec& M = models[im];
@@ -1337,7 +1352,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         const float4 b = p.ray[in_buf][1][src];
                         ow = mk3(a.x, a.y, a.z);
                         dw = mk3(b.x, b.y, b.z);
-                        winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                        winv = node_inv(cull_inv(dw));
                         dlen = sqrtf(dot(dw, dw));
                         gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
                         state = 1;
@@ -1362,7 +1377,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         const float4 b = p.ray[in_buf][1][src];
                         ow = mk3(a.x, a.y, a.z);
                         dw = mk3(b.x, b.y, b.z);
-                        winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+                        winv = node_inv(cull_inv(dw));
                         dlen = sqrtf(dot(dw, dw));
                         gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
                         state = 1;
@@ -1879,7 +1894,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         if ((phase & 1) && state == 1) {                // next model that survives culling and the grid entry test
             // world-space slopes for the instance culling: recomputed here (select steps are
             // rare) instead of living in registers through the traversal
-            const f3 winv = node_inv(mk3(1.0f / dw.x, 1.0f / dw.y, 1.0f / dw.z));
+            const f3 winv = node_inv(cull_inv(dw));
             const float dlen = sqrtf(dot(dw, dw));
             for (;;) {
                 im++;

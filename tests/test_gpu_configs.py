@@ -86,6 +86,26 @@ def test_target_1m_triangles_bitexact(gpu, pt_mod, oracle_mod, synth_dir):
     assert_bitexact(g["img"], oimg, "1M-triangle 1280x1024 image")
 
 
+@pytest.mark.parametrize("ntri,side", [(100_000, 48), (1_000_000, 16)])
+def test_bvh_mode_window_bitexact_at_size(gpu, pt_mod, oracle_mod, synth_dir, ntri, side):
+    """The exact-closest-hit mode (PT_ACCEL_BVH, bench alt_mode) at the configs[1]
+    and target scene sizes: a window of the 1280x1024 frame on the torus against
+    the oracle's exhaustive closest hit over every triangle (accel = 1)."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=ntri))
+    s.build()
+    step = 20.0 / 1280                                 # the full frame's pixel pitch (exact in binary)
+    cfg = P.RenderConfig(width=side, height=side, iterations=1, max_bounces=8, accel=P.ACCEL_BVH,
+                         plane_x0=-10.0 + 896 * step, plane_y0=-4.0 + 432 * step,
+                         plane_w=side * step, plane_h=side * step)
+    g = _gpu_render(P, s, cfg)
+    assert g["faults"] == 0
+    oimg, oseg = _oracle_render(O, s, cfg)
+    assert g["seg"] == oseg
+    assert_bitexact(g["img"], oimg, f"bvh mode, {ntri} triangles")
+
+
 def test_configs2_readme_scene_2800x2240_bitexact(gpu, pt_mod, oracle_mod):
     """configs[2]: the README render's own scene (metal, coat, diffuse and
     emissive models of Scene.cpp) at 2800x2240, the reference's 5 bounces."""
