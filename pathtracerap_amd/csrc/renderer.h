@@ -95,6 +95,9 @@ struct KParams {
                                         // hands nothing on.  Record buffers alternate between levels
     int drain_dump;                     // hand a wave's rays on once the pool is exhausted and <= this many
                                         // lanes still trace (0: off; PT_DRAIN_DUMP overrides)
+    const int4* qnodes;                 // k_trace_gf (PT_GF_QNODES): the binary BLAS with 16-bit child planes, 32 B
+                                        // per node, same indices (2 x int4: 12 planes, link|count words)
+    const float4* qframe;               // per mesh: (lo.xyz, -), (scale.xyz, -): plane = lo + q * scale
     const float4* top_nodes;            // k_trace_gf (PT_GF_TOP > 0): the top BLAS levels of mesh top_mesh, BFS
     int top_mesh;                       // order, staged in LDS (inner links into the table carry kTopFlag)
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,

@@ -21,6 +21,7 @@
 // sample -- is identical to the reference algorithm's.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1655,6 +1656,19 @@ constexpr int kCertCap = PT_CERT_CAP;
 #define PT_GF_TOP 0
 #endif
 constexpr int kGfTop = PT_GF_TOP;
+// Quantized BLAS for k_trace_gf (verdict r02 item 5a): each binary node's two child
+// boxes as 16-bit planes in its mesh's frame (plane = lo + q * scale, rounded
+// outward), links with the leaf count in the top 5 bits: 32 bytes instead of 64.
+// The slab parameter of a plane is fma(q, A, B) with A = scale / d and
+// B = (lo - o) / d per axis, set once per model; conservative like the float
+// test (the BLAS boxes carry a 1e-4-of-the-diagonal pad, the parameter's
+// rounding is far below it).  0: the float nodes.
+#ifndef PT_GF_QNODES
+#define PT_GF_QNODES 0
+#endif
+constexpr bool kGfQ = PT_GF_QNODES != 0;
+static_assert(!(kGfQ && kGfTop > 0), "PT_GF_QNODES and PT_GF_TOP are exclusive");
+constexpr int kQLinkBits = 27;
 constexpr int kTopFlag = 0x40000000;
 static_assert(kGfTop == 0 || kGfTop == 1 || kGfTop == 3 || kGfTop == 7 || kGfTop == 15, "PT_GF_TOP: whole levels");
 
@@ -1694,6 +1708,15 @@ __device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3
     const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
     tn = fmaxf(fmaxf(e0, e1), e2);
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
+    tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
+}
+
+// node_slab_g on slab parameters computed already (quantized nodes): a = entry
+// parameters of the lo planes, b = of the hi planes.
+__device__ __forceinline__ void node_slab_t(const float* a, const float* b, f3 G, float& tn, float& tf, float& tnx) {
+    const float e0 = fminf(a[0], b[0]), e1 = fminf(a[1], b[1]), e2 = fminf(a[2], b[2]);
+    tn = fmaxf(fmaxf(e0, e1), e2);
+    tf = fminf(fminf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fmaxf(a[2], b[2]));
     tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
 }
 
@@ -1745,6 +1768,14 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     float gdist = kFMax;
     int gmodel = -1, gtri = -1, im = -1;
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0), G = mk3(0, 0, 0);
+    f3 qA = mk3(0, 0, 0), qB = mk3(0, 0, 0);          // kGfQ: slab parameter = fma(q, qA, qB) per axis
+    auto set_qframe = [&](const ModelRec& M) {
+        if (kGfQ) {
+            const float4 lo = p.qframe[2 * M.mesh], sc = p.qframe[2 * M.mesh + 1];
+            qA = mk3(sc.x * ninv.x, sc.y * ninv.y, sc.z * ninv.z);
+            qB = mk3((lo.x - o.x) * ninv.x, (lo.y - o.y) * ninv.y, (lo.z - o.z) * ninv.z);
+        }
+    };
     float t_box = 0.0f, tmin = kFMax, win = 0.0f;
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
@@ -1804,6 +1835,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                         d = normalize(xform12(M.w2m, dw, 0.0f));
                         const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                         ninv = node_inv(inv);
+                        set_qframe(M);
                     }
                 } else {
                     state = 3;
@@ -1925,6 +1957,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                       !((pt.z - M.bbox[2]) < -kEps))) continue;
                 t_box = tb;
                 ninv = node_inv(inv);
+                set_qframe(M);
                 G = mk3((M.vw[0] + M.cslack[0]) * absr(ninv.x), (M.vw[1] + M.cslack[1]) * absr(ninv.y),
                         (M.vw[2] + M.cslack[2]) * absr(ninv.z));
                 if (PT_TRACE_STATS && (p.debug & 512)) G = G * 0.5f;   // timing-only ablation: half-voxel growth
@@ -2025,7 +2058,26 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
             const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
             float4 q0, q1, q2, q3;
-            if (kGfTop > 0) {
+            if (kGfQ) {
+                // 16-bit planes: child 0 lo.xyz hi.xyz, child 1 lo.xyz hi.xyz; links in w0/w1 of
+                // the second int4.  The decoded slab parameters go straight into q0..q3 in place of
+                // the planes, with an identity ray (o = 0, inv = 1) in node_slab_g below.
+                const int4 a = p.qnodes[2 * cur], b = p.qnodes[2 * cur + 1];
+                auto dq = [](int w, int hi) { return (float)(hi ? ((unsigned)w >> 16) : ((unsigned)w & 0xffffu)); };
+                q0 = make_float4(__builtin_fmaf(dq(a.x, 0), qA.x, qB.x), __builtin_fmaf(dq(a.x, 1), qA.y, qB.y),
+                                 __builtin_fmaf(dq(a.y, 0), qA.z, qB.z), 0.0f);
+                q1 = make_float4(__builtin_fmaf(dq(a.y, 1), qA.x, qB.x), __builtin_fmaf(dq(a.z, 0), qA.y, qB.y),
+                                 __builtin_fmaf(dq(a.z, 1), qA.z, qB.z), 0.0f);
+                q2 = make_float4(__builtin_fmaf(dq(a.w, 0), qA.x, qB.x), __builtin_fmaf(dq(a.w, 1), qA.y, qB.y),
+                                 __builtin_fmaf(dq(b.x, 0), qA.z, qB.z), 0.0f);
+                q3 = make_float4(__builtin_fmaf(dq(b.x, 1), qA.x, qB.x), __builtin_fmaf(dq(b.y, 0), qA.y, qB.y),
+                                 __builtin_fmaf(dq(b.y, 1), qA.z, qB.z), 0.0f);
+                const int lmask = (1 << kQLinkBits) - 1;
+                q0.w = __int_as_float(b.z & lmask);
+                q1.w = __int_as_float(b.w & lmask);
+                q2.w = __int_as_float((int)((unsigned)b.z >> kQLinkBits) - 1);
+                q3.w = __int_as_float((int)((unsigned)b.w >> kQLinkBits) - 1);
+            } else if (kGfTop > 0) {
                 // staged slot: an unconditional LDS read (clamped slot), the global node only for
                 // the lanes below the table (typed pointers keep the two loads apart)
                 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -2052,8 +2104,13 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
             const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
             float tn0, tf0, tn1, tf1, tx0, tx1;
-            node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
-            node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
+            if (kGfQ) {                                 // q0..q3 hold slab parameters already
+                node_slab_t(lo0, hi0, G, tn0, tf0, tx0);
+                node_slab_t(lo1, hi1, G, tn1, tf1, tx1);
+            } else {
+                node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
+                node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
+            }
             const float X = tmin + win;
             const float bound = X + gf_slack(X, t_box);
             // non-short-circuit: both children's slabs in one basic block (a branch on
@@ -2816,6 +2873,84 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr;
     kp.top_nodes = nullptr;
     kp.top_mesh = -1;
+    kp.qnodes = nullptr;
+    kp.qframe = nullptr;
+    if (kGfQ && cfg.accel == ACCEL_GRID_FAST) {
+        // 32-byte quantized copy of the binary BLAS (same node indices), per mesh frame
+        const size_t nn = scene.bvh_nodes.size();
+        std::vector<int4> q(2 * nn, make_int4(0, 0, 0, 0));
+        std::vector<float4> frame(2 * scene.meshes.size(), make_float4(0, 0, 0, 0));
+        for (size_t m = 0; m < scene.meshes.size(); m++) {
+            const int root = scene.mesh_bvh_root[m];
+            if (root < 0) continue;
+            std::vector<int> order{root};
+            double flo[3] = {1e300, 1e300, 1e300}, fhi[3] = {-1e300, -1e300, -1e300};
+            for (size_t i = 0; i < order.size(); i++) {
+                const BvhNode& nd = scene.bvh_nodes[order[i]];
+                const int cnt[2] = {nd.count0, nd.count1};
+                const float* lo[2] = {nd.lo0, nd.lo1};
+                const float* hi[2] = {nd.hi0, nd.hi1};
+                for (int c = 0; c < 2; c++) {
+                    if (cnt[c] < 0) continue;
+                    for (int k = 0; k < 3; k++) { flo[k] = std::min(flo[k], (double)lo[c][k]); fhi[k] = std::max(fhi[k], (double)hi[c][k]); }
+                }
+                if (nd.count0 == 0) order.push_back(nd.link0);
+                if (nd.count1 == 0) order.push_back(nd.link1);
+            }
+            float fl[3], sc[3];
+            for (int k = 0; k < 3; k++) {
+                if (!(flo[k] <= fhi[k]) || !std::isfinite(flo[k]) || !std::isfinite(fhi[k])) {
+                    last_error = "quantized BLAS: mesh box not finite";
+                    return -1;
+                }
+                fl[k] = (float)flo[k];
+                if ((double)fl[k] > flo[k]) fl[k] = std::nextafter(fl[k], -INFINITY);
+                sc[k] = (float)std::max((fhi[k] - (double)fl[k]) / 65535.0, 1e-30);
+                while ((double)fl[k] + 65535.0 * (double)sc[k] < fhi[k]) sc[k] = std::nextafter(sc[k], INFINITY);
+            }
+            frame[2 * m] = make_float4(fl[0], fl[1], fl[2], 0.0f);
+            frame[2 * m + 1] = make_float4(sc[0], sc[1], sc[2], 0.0f);
+            auto qlo = [&](float v, int k) {
+                double x = std::floor(((double)v - fl[k]) / sc[k]);
+                x = std::min(std::max(x, 0.0), 65535.0);
+                while (x > 0 && (double)fl[k] + x * (double)sc[k] > (double)v) x -= 1.0;
+                return (unsigned)x;
+            };
+            auto qhi = [&](float v, int k) {
+                double x = std::ceil(((double)v - fl[k]) / sc[k]);
+                x = std::min(std::max(x, 0.0), 65535.0);
+                while (x < 65535.0 && (double)fl[k] + x * (double)sc[k] < (double)v) x += 1.0;
+                return (unsigned)x;
+            };
+            for (int n : order) {
+                const BvhNode& nd = scene.bvh_nodes[n];
+                unsigned w[6] = {0, 0, 0, 0, 0, 0};
+                const int cnt[2] = {nd.count0, nd.count1};
+                const int link[2] = {nd.link0, nd.link1};
+                const float* lo[2] = {nd.lo0, nd.lo1};
+                const float* hi[2] = {nd.hi0, nd.hi1};
+                unsigned v[12];
+                for (int c = 0; c < 2; c++)
+                    for (int k = 0; k < 3; k++) {
+                        v[6 * c + k] = cnt[c] >= 0 ? qlo(lo[c][k], k) : 1;
+                        v[6 * c + 3 + k] = cnt[c] >= 0 ? qhi(hi[c][k], k) : 0;
+                    }
+                for (int i = 0; i < 6; i++) w[i] = v[2 * i] | (v[2 * i + 1] << 16);
+                int lw[2];
+                for (int c = 0; c < 2; c++) {
+                    if (cnt[c] + 1 >= 32 || (cnt[c] >= 0 && (link[c] < 0 || link[c] >= (1 << kQLinkBits)))) {
+                        last_error = "quantized BLAS: link or leaf count out of range";
+                        return -1;
+                    }
+                    lw[c] = (cnt[c] < 0 ? 0 : link[c]) | ((cnt[c] + 1) << kQLinkBits);
+                }
+                q[2 * (size_t)n] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+                q[2 * (size_t)n + 1] = make_int4((int)w[4], (int)w[5], lw[0], lw[1]);
+            }
+        }
+        PT_HIP(upload(allocs, &kp.qnodes, q.data(), q.size() * sizeof(int4), stream));
+        PT_HIP(upload(allocs, &kp.qframe, frame.data(), frame.size() * sizeof(float4), stream));
+    }
     if (kGfTop > 0 && cfg.accel == ACCEL_GRID_FAST) {
         // k_trace_gf's LDS table: the first kGfTop nodes, breadth first, of the BLAS of the
         // mesh with the most triangles; inner links into the table become kTopFlag | slot

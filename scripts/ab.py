@@ -27,11 +27,12 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--scene", default=None, help="scene file instead of the synthetic one")
+    ap.add_argument("--inmem", action="store_true", help="the synthetic scene built in memory (no OBJ text: 10M triangles)")
     a = ap.parse_args()
     import torch
     import pathtracerap_amd as P
     from pathtracerap_amd import synthetic
-    path = a.scene or synthetic.diffuse_scene(tempfile.mkdtemp(), ntri=a.ntri)
+    path = a.scene or (None if a.inmem else synthetic.diffuse_scene(tempfile.mkdtemp(), ntri=a.ntri))
     scenes = {}
     rs = {}
     for v in a.variants:
@@ -42,8 +43,11 @@ def main():
         os.environ.update(env)          # read by allocateOnGPU
         acc = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[accel]
         if acc not in scenes:
-            s = P.Scene(path)
-            s.build(bvh=acc != P.ACCEL_GRID)
+            if a.inmem and not a.scene:
+                s = synthetic.build_scene(P, ntri=a.ntri)
+            else:
+                s = P.Scene(path)
+                s.build(bvh=acc != P.ACCEL_GRID)
             scenes[acc] = s
         cfg = P.RenderConfig(width=a.width, height=a.height, max_bounces=a.bounces, accel=acc, block=int(block))
         r = P.Renderer(cfg)

@@ -496,9 +496,20 @@ def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypat
     s = P.Scene(path)
     s.build(bvh=True)
     cfg = P.RenderConfig(width=173, height=89, iterations=3, max_bounces=7, accel=P.ACCEL_GRID_FAST, pipelines=pipes)
-    img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+    r = P.Renderer(cfg)
+    r.allocateOnGPU(s)
+    r.renderLoop()
+    img, seg, deferred = r.image(), r.segments(), r.deferred_rays()
+    r.free()
+    oimg, oseg = O.render(flat_from_export(s.export(), cfg.grid), oracle_cfg(cfg))
     assert seg == oseg
     assert_bitexact(img, oimg, f"PT_WALK_HANDON={handon} PT_WALK_WCAP={wcap} pipes={pipes} {scene}")
+    # the route the undecided walks took: in place (handon=0) or handed on with room for
+    # all of them -> nothing reaches k_trace_deferred; 7 records -> the rest go there
+    if wcap is None:
+        assert deferred == 0, deferred
+    else:
+        assert deferred > 0
 
 
 @pytest.mark.parametrize("accel", [1, 2])
