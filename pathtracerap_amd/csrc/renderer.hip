@@ -210,7 +210,7 @@ __device__ bool grid_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3
 // are padded by 1e-4 of their diagonal + 0.01 (plus 1e-3 of the mesh diagonal
 // + 1 before the transform), far beyond a few ulps of the slab parameters.
 #ifndef PT_CULL_RCP
-#define PT_CULL_RCP 1
+#define PT_CULL_RCP 0       // measured neutral (README scene -0.5 % / +0.5 %): exact divisions stay
 #endif
 __device__ __forceinline__ f3 cull_inv(f3 d) {
     if (PT_CULL_RCP) return mk3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
@@ -1218,6 +1218,7 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 #define PT_LDS_MODELS_BVH 8
 #endif
 constexpr int kLdsModels = PT_LDS_MODELS_BVH;
+constexpr int kLdsModelsWide = 12;
 constexpr int kLdsModelsGf = PT_LDS_MODELS_GF;
 constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
 
@@ -1245,7 +1246,10 @@ template <int BS, int F, bool TAIL = false>
 __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, int bounce, int level) {
     static_assert(kCX + 3 + kStack <= kContFields, "continuation record too small");
     __shared__ int s_stack[kStack * BS];
-    __shared__ ModelRec s_models[(F & 1) ? kLdsModels : 1];
+    // F & 32: room for kLdsModelsWide records (scenes of 9..12 models: 17 resident waves per CU
+    // instead of 20, but no model reads from global memory: README scene +6 %)
+    constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModels) : 1;
+    __shared__ ModelRec s_models[kModelsHere];
     int* stack = s_stack + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
     int* spill = p.spill + sbase;                        // stack entries beyond the LDS part
@@ -1263,7 +1267,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     if (lds_models) {
         const int* src = reinterpret_cast<const int*>(p.models);
         int* dst = reinterpret_cast<int*>(s_models);
-        const int nw = min(p.nmodels, kLdsModels) * (int)(sizeof(ModelRec) / 4);
+        const int nw = min(p.nmodels, kModelsHere) * (int)(sizeof(ModelRec) / 4);
         for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
         __syncthreads();
     }
@@ -2809,6 +2813,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
         kp.trace_flags = tf ? std::atoi(tf) : 11;
+        // the default variant with 9..12 models: model records in LDS with room for 12 (F | 32)
+        bvh_wide_lds = (kp.trace_flags & 31) == 11 && scene.model_recs.size() > (size_t)kLdsModels &&
+                       scene.model_recs.size() <= (size_t)kLdsModelsWide;
         if (scene.model_recs.size() > (size_t)kLdsModels) kp.trace_flags &= ~1;
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3109,7 +3116,8 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
         hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, PT_DEFER_WGS)), t, 0, st, k, b);
         return;
     }
-    switch (k.trace_flags & 31) {
+    switch (bvh_wide_lds ? 43 : (k.trace_flags & 31)) {
+        case 43: hipLaunchKernelGGL((k_trace_bvh<64, 43>), g, t, 0, st, k, b, 0); break;   // 11 with 9..12 models
         case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, st, k, b, 0); break;
         case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, st, k, b, 0); break;
         case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, st, k, b, 0); break;
@@ -3135,6 +3143,7 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             else hipLaunchKernelGGL((k_trace_bvh<64, 26, true>), g, t, 0, st, k, b, l);
         } else {
             if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b, l);
+            else if (bvh_wide_lds) hipLaunchKernelGGL((k_trace_bvh<64, 43, true>), g, t, 0, st, k, b, l);
             else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b, l);
         }
     }
