@@ -1394,7 +1394,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
         }
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
-        if (iters > p.trace_iter_cap) {                 // safety net: never spin forever (reported as a fault)
+        // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
+        // the cap's kernel-argument load stays out of the loop's common path
+        if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
             if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
             break;
         }
@@ -1898,7 +1900,9 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
         }
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
-        if (iters > p.trace_iter_cap) {                 // safety net: never spin forever (reported as a fault)
+        // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
+        // the cap's kernel-argument load stays out of the loop's common path
+        if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
             if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
             break;
         }

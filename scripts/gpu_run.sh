@@ -14,6 +14,7 @@
 #   ab=ARGS               python scripts/ab.py ARGS (interleaved in-process A/B)
 #   ablib=R@SPEC@N1,N2    R interleaved rounds of ab.py SPEC over library builds
 #                         (build_variants/lib_N.so from scripts/build_variant.sh; "default" = in-tree)
+#   abbench=R@ARGS@N1,N2  R interleaved rounds of bench.py ARGS (main line only) over library builds
 #   py=SCRIPT ARGS        python SCRIPT ARGS (a measurement script under scripts/)
 #
 # Example: bash scripts/gpu_run.sh tests "bench=--steps 32" "prof=--pipelines 1 --targets= --no-cpu-baseline"
@@ -75,6 +76,17 @@ for step in "$@"; do
           PT_LIB_PATH=$L timeout -k 10 300 python scripts/ab.py --variants $spec --rounds 2 --steps 16 > gpurun_out/${tag}_$lib.json 2> gpurun_out/${tag}_$lib.err
           rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/${tag}_$lib.err; break 2; }
           python3 -c "import json; d=json.load(open('gpurun_out/${tag}_$lib.json')); print('round $r $lib', {k: v['Mrays_s'] for k, v in d.items()})"
+        done
+      done ;;
+    abbench)
+      IFS=@ read -r rounds bargs names <<< "$arg"
+      rc=0
+      for r in $(seq 1 "$rounds"); do
+        for lib in ${names//,/ }; do
+          if [ "$lib" = default ]; then L=$PWD/pathtracerap_amd/libpathtracer_amd.so; else L=$PWD/build_variants/lib_$lib.so; fi
+          PT_LIB_PATH=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile --alt-accel= --targets= $bargs > gpurun_out/${tag}_$lib.json 2> gpurun_out/${tag}_$lib.err
+          rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/${tag}_$lib.err; break 2; }
+          python3 -c "import json; d=json.load(open('gpurun_out/${tag}_$lib.json')); print('round $r $lib', d['value'], d['ms_per_step'])"
         done
       done ;;
     py)

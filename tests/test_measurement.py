@@ -62,3 +62,34 @@ def test_committed_pmc_summary_has_bench_keys():
         assert e[kern]["hbm_bytes_per_launch"] > 0
         assert e["_sq"]["valu_insts_per_iteration"] > 0
         assert e["_sq_p1"]["kernels"][kern]["valu_insts_per_launch"] > 0
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_bench_rates_and_roofline_bytes():
+    """bench.py's arithmetic: segment rate with and without the cached primary
+    bounce, samples/s over all ranks, and the trace's algorithmic bytes per step
+    (52 B per segment entering bounce >= 1)."""
+    b = _bench()
+    res = {"elapsed": 2.0, "seg": 8.0e9, "seg_primary": 2.0e9}
+    r = b.rates(res, K=100, npix=1000, world=2)
+    assert r["value"] == 4000.0 and r["traced_mrays_per_sec"] == 3000.0
+    assert r["ms_per_step"] == 20.0 and r["samples_per_sec"] == 100.0
+    assert b.trace_bytes_per_step([10, 6, 4, 0], K=2) == 52.0 * 10 / 2
+    assert b.VALU_PEAK_G == 256 * 4 * 2.4 / 2
+
+
+def test_bench_workload_labels():
+    b = _bench()
+    import argparse
+    a = argparse.Namespace(scene="", ntri=100_000, width=1280, height=1024, bounces=8, metallic=False)
+    assert b.workload_name(a).startswith("configs[1]")
+    a.ntri = 1_000_000
+    assert b.workload_name(a).startswith("north_star target")
+    a.ntri, a.bounces = 10_000_000, 16
+    assert b.workload_name(a).startswith("configs[4]")
