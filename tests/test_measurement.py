@@ -79,7 +79,7 @@ def test_bench_rates_and_roofline_bytes():
     res = {"elapsed": 2.0, "seg": 8.0e9, "seg_primary": 2.0e9}
     r = b.rates(res, K=100, npix=1000, world=2)
     assert r["value"] == 4000.0 and r["traced_mrays_per_sec"] == 3000.0
-    assert r["ms_per_step"] == 20.0 and r["samples_per_sec"] == 100.0
+    assert r["ms_per_step"] == 20.0 and r["samples_per_sec"] == 2 * 100 * 1000 / 2.0
     assert b.trace_bytes_per_step([10, 6, 4, 0], K=2) == 52.0 * 10 / 2
     assert b.VALU_PEAK_G == 256 * 4 * 2.4 / 2
 
