@@ -182,6 +182,7 @@ private:
     bool split_trace = false;        // persistent k_trace_bvh / k_trace_gf + shading pass
     int trace_blocks = 0;
     int gf_flags = 9;                // k_trace_gf variant: 1 LDS model records, 8 phase scheduling
+    bool gf_wide_lds = false;        // k_trace_gf default variants with 9..12 models: 12 LDS records (F | 32)
     bool bvh_wide_lds = false;       // k_trace_bvh default variant with 9..12 models: 12 LDS records (F = 43)
     KernelStats stats;
 };

@@ -1209,10 +1209,13 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
 #define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
 #endif
 // Model records staged in LDS when the scene has at most this many: k_trace_gf
-// 12 (7168 B of lane state + 12 x 248 B = 10144 B per 64-lane workgroup, 16 per
-// CU), k_trace_bvh 8 (6144 + 8 x 248 = 8128 B, 20 per CU).
+// 8 (7168 B of lane state + 8 x 248 B = 9152 B per 64-lane workgroup), or 12 for
+// scenes of 9..12 instances (variant F | 32: 10144 B, still 16 per CU; the
+// smaller table leaves LDS room beside 16 trace workgroups for the other
+// pipelines' small kernels: 1 % at configs[1]); k_trace_bvh 8 (6144 + 8 x 248
+// = 8128 B, 20 per CU), 12 with F | 32 (9120 B, 17 per CU).
 #ifndef PT_LDS_MODELS_GF
-#define PT_LDS_MODELS_GF 12
+#define PT_LDS_MODELS_GF 8
 #endif
 #ifndef PT_LDS_MODELS_BVH
 #define PT_LDS_MODELS_BVH 8
@@ -1731,7 +1734,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     static_assert(kCX + 9 + kGfStack + 4 * kGfHitCap <= kContFields, "continuation record too small");
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
-    __shared__ ModelRec s_models[(F & 1) ? kLdsModelsGf : 1];
+    constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModelsGf) : 1;
+    __shared__ ModelRec s_models[kModelsHere];
     __shared__ float4 s_top[kGfTop > 0 ? 4 * kGfTop : 1];
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
@@ -1753,7 +1757,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     if (lds_models) {
         const int* src = reinterpret_cast<const int*>(p.models);
         int* dst = reinterpret_cast<int*>(s_models);
-        const int nw = min(p.nmodels, kLdsModelsGf) * (int)(sizeof(ModelRec) / 4);
+        const int nw = min(p.nmodels, kModelsHere) * (int)(sizeof(ModelRec) / 4);
         for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
         __syncthreads();
     }
@@ -2812,7 +2816,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
         const char* gff = std::getenv("PT_GF_FLAGS");
         gf_flags = gff ? std::atoi(gff) : 9;
-        if (scene.model_recs.size() > (size_t)kLdsModelsGf) gf_flags &= ~1;   // model records stay in global memory
+        // 9..12 instances: the default variants with room for 12 LDS model records (F | 32)
+        gf_wide_lds = (gf_flags & ~1) == 8 && (gf_flags & 1) && scene.model_recs.size() > (size_t)kLdsModelsGf &&
+                      scene.model_recs.size() <= (size_t)kLdsModelsWide;
+        if (scene.model_recs.size() > (size_t)kLdsModelsGf && !gf_wide_lds) gf_flags &= ~1;   // records stay global
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
@@ -3093,8 +3100,9 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
         // model records in LDS: the variant asks for them (gf_flags & 1, cleared by
-        // allocateOnGPU when the scene has more than kLdsModelsGf models)
+        // allocateOnGPU when the scene has more models than the tables hold)
         const bool lds = (gf_flags & 1) && k.nmodels <= kLdsModelsGf;
+        const bool wide = gf_wide_lds;                  // 9..12 models: the 12-record variants
         switch (gf_flags) {
             case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b, 0); break;
             case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b, 0); break;
@@ -3104,9 +3112,11 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
                                              // launch with walk hand-ons, else (| 16) walks in place
                 if (k.cont_wcap > 0) {
                     if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
+                    else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 41>), g, t, 0, st, k, b, 0);
                     else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
                 } else {
                     if (lds) hipLaunchKernelGGL((k_trace_gf<64, 25>), g, t, 0, st, k, b, 0);
+                    else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 57>), g, t, 0, st, k, b, 0);
                     else hipLaunchKernelGGL((k_trace_gf<64, 24>), g, t, 0, st, k, b, 0);
                 }
                 break;
@@ -3114,6 +3124,7 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
         for (int l = 1; (k.drain_dump > 0 && l <= k.drain_levels) || (k.cont_wcap > 0 && l == 1); l++) {
             // the rays handed on (drain continuations; walk hand-ons go to level 1), packed
             if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b, l);
+            else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 41, true>), g, t, 0, st, k, b, l);
             else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b, l);
         }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
