@@ -1196,18 +1196,6 @@ __device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 in
     return n;
 }
 
-// Pipelined refill of the main persistent traces.  A refill is three dependent
-// round trips (the claim atomic, the sorted-order entry, the ray); done in one
-// go, the whole wave -- its busy lanes too -- waits for all three.  With
-// PT_REFILL_PIPE each round trip is issued at the top of one loop iteration and
-// consumed at the top of the next, so it overlaps that iteration's traversal
-// step (whose own loads the wave waits for anyway): idle lanes pass through
-// states 7 (claimed), 8 (order entry loaded), 9 (ray loaded) before selecting.
-// One claim is in flight per wave; the drain waits until no lane is in flight.
-#ifndef PT_REFILL_PIPE
-#define PT_REFILL_PIPE 0
-#endif
-constexpr bool kRefillPipe = PT_REFILL_PIPE != 0;
 #ifndef PT_LEAF_STEP
 #define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of k_trace_bvh (1..4; k_trace_gf: 1 or 2)
 #endif
@@ -1310,61 +1298,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
     int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // wave's claimed source block (uniform)
-    // pipelined refill (PT_REFILL_PIPE, above): states 7 claimed, 8 order entry, 9 ray loaded
-    constexpr bool pipe = kRefillPipe && !TAIL && !(F & 4);
-    int cl_ret = 0;
-    bool cl_pend = false, st8 = false, st9 = false;
-    int cl_leader = 0, cl_cnt = 0;
-    unsigned long long cl_mask = 0;
     for (unsigned iters = 0;; iters++) {
-        if (pipe && (cl_pend | st8 | st9)) {
-            if (st9) {
-                if (state == 9) {
-                    winv = node_inv(cull_inv(dw));
-                    dlen = sqrtf(dot(dw, dw));
-                    state = 1;
-                }
-                st9 = false;
-            }
-            if (st8) {
-                if (state == 8) {                   // cur holds the source index
-                    const float4 a = p.ray[in_buf][0][cur];
-                    const float4 b = p.ray[in_buf][1][cur];
-                    ow = mk3(a.x, a.y, a.z);
-                    dw = mk3(b.x, b.y, b.z);
-                    state = 9;
-                }
-                st8 = false; st9 = true;
-            }
-            if (cl_pend) {
-                const int base = __builtin_amdgcn_readlane(cl_ret, cl_leader);   // uniform: SGPR
-                if (base + cl_cnt >= n) exhausted = true;
-                if (state == 7) {
-                    j = base + __popcll(cl_mask & ((1ull << lane) - 1ull));
-                    if (j < n) {
-                        if (p.order) { const int2 e = p.order[j]; j = p.hit_order ? j : e.x; cur = e.y; }
-                        else cur = slot_source(p, j);
-                        gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                        state = 8;
-                    } else {
-                        state = 3;
-                    }
-                }
-                cl_pend = false; st8 = true;
-            }
-        }
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (pipe) {
-            if (!cl_pend && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
-                cl_cnt = __popcll(idle);
-                cl_leader = __ffsll((long long)idle) - 1;
-                cl_mask = idle;
-                if (lane == cl_leader) cl_ret = atomicAdd(p.trace_next, cl_cnt);
-                cl_pend = true;
-                if (state == 0) state = 7;
-            }
-        } else if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             if (TAIL) {                                     // resume continuation records
                 const int cnt = __popcll(idle);
                 const int leader = __ffsll((long long)idle) - 1;
@@ -1477,9 +1414,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             if (c1 * 4 > cm * PT_BVH_SEL_W) phase = 1;
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
-        if (may_dump && exhausted && p.drain_dump > 0 && !(pipe && (cl_pend | st8 | st9)) &&
-            __popcll(__ballot(state != 3)) <= p.drain_dump)
-            phase = 16;
+        if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
@@ -1864,54 +1799,10 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
     unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
-    constexpr bool pipe = kRefillPipe && !TAIL && !(F & 4);
-    int cl_ret = 0;                                 // pipe: the claim atomic's return (leader lane)
-    bool cl_pend = false, st8 = false, st9 = false; // pipe (uniform): a claim / order loads / ray loads in flight
-    int cl_leader = 0, cl_cnt = 0;
-    unsigned long long cl_mask = 0;
     for (unsigned iters = 0;; iters++) {
-        if (pipe && (cl_pend | st8 | st9)) {
-            // later stages first, so a lane advances one stage per iteration
-            if (st9) { if (state == 9) state = 1; st9 = false; }
-            if (st8) {
-                if (state == 8) {                   // cur holds the source index
-                    const float4 a = p.ray[in_buf][0][cur];
-                    const float4 b = p.ray[in_buf][1][cur];
-                    ow = mk3(a.x, a.y, a.z);
-                    dw = mk3(b.x, b.y, b.z);
-                    state = 9;
-                }
-                st8 = false; st9 = true;
-            }
-            if (cl_pend) {
-                const int base = __builtin_amdgcn_readlane(cl_ret, cl_leader);   // uniform: SGPR
-                if (base + cl_cnt >= n) exhausted = true;
-                if (state == 7) {
-                    j = base + __popcll(cl_mask & ((1ull << lane) - 1ull));
-                    if (j < n) {
-                        if (p.order) { const int2 e = p.order[j]; j = p.hit_order ? j : e.x; cur = e.y; }
-                        else cur = slot_source(p, j);
-                        gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                        state = 8;
-                    } else {
-                        state = 3;
-                    }
-                }
-                cl_pend = false; st8 = true;
-            }
-        }
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (pipe) {
-            if (!cl_pend && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
-                cl_cnt = __popcll(idle);
-                cl_leader = __ffsll((long long)idle) - 1;
-                cl_mask = idle;
-                if (lane == cl_leader) cl_ret = atomicAdd(p.trace_next, cl_cnt);
-                cl_pend = true;
-                if (state == 0) state = 7;
-            }
-        } else if (TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        if (TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             // resume continuation records
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
@@ -2029,10 +1920,7 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
             if (c1 * 4 > cm * PT_SEL_W) { phase = 1; cm = c1; }
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
-        // (pipe: not while a refill is in flight -- its lanes carry no traversal state yet)
-        if (may_dump && exhausted && p.drain_dump > 0 && !(pipe && (cl_pend | st8 | st9)) &&
-            __popcll(__ballot(state != 3)) <= p.drain_dump)
-            phase = 16;
+        if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
