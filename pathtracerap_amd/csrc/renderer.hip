@@ -87,6 +87,50 @@ constexpr int kScanWG = PT_SCAN_WG, kScanPer = 8;                   // k_scan: o
 // ---------------------------------------------------------------------------
 struct Hit { float dist; f3 n; int model; };
 
+// Streaming (non-temporal) access to the ray pools (PT_RAY_NT bits): 1 the
+// persistent traces' refill gathers (ray + claim-order entry), 2 the shading
+// pass's ray / hit reads and ray writes, 4 the sort's ray reads.  Ray data is
+// touched once per pass; marked non-temporal it need not displace the BLAS
+// lines the traces re-read from L2.
+#ifndef PT_RAY_NT
+#define PT_RAY_NT 0
+#endif
+// Ray pool layout (PT_RAY_AOS): 0 = planes (o, pixel) and (d, bounces) apart (two
+// L2 lines per ray gathered by a trace refill); 1 = the two interleaved per ray, 32
+// contiguous bytes (one line).  Plane q of ray i is p.ray[buf][q][kRS * i].
+#ifndef PT_RAY_AOS
+#define PT_RAY_AOS 0
+#endif
+constexpr int kRS = PT_RAY_AOS ? 2 : 1;
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+template <int BIT>
+__device__ __forceinline__ float4 ld_ray(const float4* q) {
+    if (PT_RAY_NT & BIT) {
+        const v4f_t v = __builtin_nontemporal_load(reinterpret_cast<const v4f_t*>(q));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    return *q;
+}
+template <int BIT>
+__device__ __forceinline__ int2 ld_ord(const int2* q) {
+    if (PT_RAY_NT & BIT) {
+        const v2i_t v = __builtin_nontemporal_load(reinterpret_cast<const v2i_t*>(q));
+        return make_int2(v.x, v.y);
+    }
+    return *q;
+}
+template <int BIT>
+__device__ __forceinline__ void st_ray(float4* q, float4 v) {
+    if (PT_RAY_NT & BIT) {
+        v4f_t w;
+        w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+        __builtin_nontemporal_store(w, reinterpret_cast<v4f_t*>(q));
+    } else {
+        *q = v;
+    }
+}
+
 // computeRayBoundingBoxIntersection (Renderer.cpp:150-170)
 __device__ __forceinline__ bool slab_ref(const float* bb, f3 o, f3 d, f3 inv, float& t) {
     float t1 = d.x == 0.0f ? kFMin : (bb[0] - o.x) * inv.x;
@@ -1356,8 +1400,8 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     if (state == 0 && rank < take) {
                         const int src = q_b * CH + q_pos + rank;
                         j = q_off + q_pos + rank;
-                        const float4 a = p.ray[in_buf][0][src];
-                        const float4 b = p.ray[in_buf][1][src];
+                        const float4 a = p.ray[in_buf][0][kRS * src];
+                        const float4 b = p.ray[in_buf][1][kRS * src];
                         ow = mk3(a.x, a.y, a.z);
                         dw = mk3(b.x, b.y, b.z);
                         winv = node_inv(cull_inv(dw));
@@ -1379,10 +1423,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     j = base + __popcll(idle & ((1ull << lane) - 1ull));
                     if (j < n) {
                         int src;
-                        if (p.order) { const int2 e = p.order[j]; j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
+                        if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
                         else src = slot_source(p, j);
-                        const float4 a = p.ray[in_buf][0][src];
-                        const float4 b = p.ray[in_buf][1][src];
+                        const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
+                        const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
                         ow = mk3(a.x, a.y, a.z);
                         dw = mk3(b.x, b.y, b.z);
                         winv = node_inv(cull_inv(dw));
@@ -1652,6 +1696,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_MINWAVES
 #define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
 #endif
+#ifndef PT_GF_TAIL_MINWAVES
+#define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
+#endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
 #ifndef PT_CERT_CAP
 #define PT_CERT_CAP PT_GF_HITCAP   // members the main launch's walk certificate handles (walk hand-ons: the rest)
@@ -1730,7 +1777,7 @@ __device__ __forceinline__ void node_slab_t(const float* a, const float* b, f3 G
 }
 
 template <int BS, int F, bool TAIL = false>
-__global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce, int level) {
+__global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce, int level) {
     static_assert(kCX + 9 + kGfStack + 4 * kGfHitCap <= kContFields, "continuation record too small");
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
@@ -1868,8 +1915,8 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 if (state == 0 && rank < take) {
                     const int src = q_b * p.chunk + q_pos + rank;
                     j = q_off + q_pos + rank;
-                    const float4 a = p.ray[in_buf][0][src];
-                    const float4 b = p.ray[in_buf][1][src];
+                    const float4 a = p.ray[in_buf][0][kRS * src];
+                    const float4 b = p.ray[in_buf][1][kRS * src];
                     ow = mk3(a.x, a.y, a.z);
                     dw = mk3(b.x, b.y, b.z);
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
@@ -1889,10 +1936,10 @@ __global__ __launch_bounds__(BS, PT_GF_MINWAVES) void k_trace_gf(KParams p, int 
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
                     int src;
-                    if (p.order) { const int2 e = p.order[j]; j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
+                    if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
                     else src = slot_source(p, j);
-                    const float4 a = p.ray[in_buf][0][src];
-                    const float4 b = p.ray[in_buf][1][src];
+                    const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
+                    const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
                     ow = mk3(a.x, a.y, a.z);
                     dw = mk3(b.x, b.y, b.z);
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
@@ -2300,8 +2347,8 @@ __global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
     for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
         const int j = p.defer_slots[q];              // hit_order: the claim position
         const int src = p.hit_order ? p.order[j].y : slot_source(p, j);
-        const float4 a = p.ray[in_buf][0][src];
-        const float4 b = p.ray[in_buf][1][src];
+        const float4 a = p.ray[in_buf][0][kRS * src];
+        const float4 b = p.ray[in_buf][1][kRS * src];
         const Hit h = intersect_scene<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
                                                            s_stack + threadIdx.x, s_hs + threadIdx.x);
         p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
@@ -2358,15 +2405,15 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
                 }
                 src = lo * BS + (j - p.blk_off[lo]);
             }
-            const float4 a = p.ray[in_buf][0][src];
-            const float4 b = p.ray[in_buf][1][src];
-            const float4 c = p.ray[in_buf][2][src];
+            const float4 a = ld_ray<2>(p.ray[in_buf][0] + kRS * src);
+            const float4 b = ld_ray<2>(p.ray[in_buf][1] + kRS * src);
+            const float4 c = ld_ray<2>(p.ray[in_buf][2] + src);
             r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
             r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
             r.c = mk3(c.x, c.y, c.z);
             if (ACCEL == kAccelHitBuffer) {       // traced by k_trace_bvh / k_trace_gf
                 const int hj = p.hit_order ? p.slot_pos[j] : j;   // hit_order: records sit in claim order
-                const float4 hh = p.hit4[hj];
+                const float4 hh = ld_ray<2>(p.hit4 + hj);
                 h.dist = hh.x;
                 h.n = mk3(hh.y, hh.z, hh.w);
                 h.model = p.hitm[hj];
@@ -2414,9 +2461,9 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
     }
     if (alive) {
         const int dst = j0 + base + rank;
-        p.ray[out_buf][0][dst] = make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(r.pixel));
-        p.ray[out_buf][1][dst] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(r.bounces));
-        p.ray[out_buf][2][dst] = make_float4(r.c.x, r.c.y, r.c.z, 0.0f);
+        st_ray<2>(p.ray[out_buf][0] + kRS * dst, make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(r.pixel)));
+        st_ray<2>(p.ray[out_buf][1] + kRS * dst, make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(r.bounces)));
+        st_ray<2>(p.ray[out_buf][2] + dst, make_float4(r.c.x, r.c.y, r.c.z, 0.0f));
     }
     if (threadIdx.x == 0) p.blk_cnt[chunk] = total;
 }
@@ -2590,8 +2637,8 @@ __global__ __launch_bounds__(kSortWG) void k_sort_hist(KParams p, int bounce) {
         if (i < lim) {
             const int c = i / p.chunk, r = i - c * p.chunk;
             if (r < p.blk_cnt[c]) {
-                const float4 a = p.ray[in_buf][0][i];
-                const float4 b = p.ray[in_buf][1][i];
+                const float4 a = ld_ray<4>(p.ray[in_buf][0] + kRS * i);
+                const float4 b = ld_ray<4>(p.ray[in_buf][1] + kRS * i);
                 const int key = sort_key(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
                 p.sort_key[i] = (unsigned short)key;
                 atomicAdd(&s_h[key], 1);
@@ -3034,7 +3081,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
 // spill, hit buffer and work counters.
 int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     for (int b = 0; b < 2; b++)
-        for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &k.ray[b][q], nullptr, cap * sizeof(float4), st));
+        for (int q = 0; q < 3; q++) {
+            if (q == 1 && kRS == 2) { k.ray[b][1] = k.ray[b][0] + 1; continue; }   // interleaved with plane 0
+            PT_HIP(upload(allocs, &k.ray[b][q], nullptr, (q < 2 ? kRS : 1) * cap * sizeof(float4), st));
+        }
     PT_HIP(upload(allocs, &k.blk_cnt, nullptr, (k.nblocks + 1) * sizeof(int), st));
     PT_HIP(upload(allocs, &k.blk_off, nullptr, (k.nblocks + 2) * sizeof(int), st));
     PT_HIP(upload(allocs, &k.dst_start, nullptr, (k.nblocks + 2) * sizeof(int), st));
