@@ -46,6 +46,9 @@ constexpr int kBlock = 256;
 #ifndef PT_CERT_FILTER
 #define PT_CERT_FILTER 1      // walk certificate: U over the members not provably entered after B* (walk_certify)
 #endif
+#ifndef PT_CERT_INSIDE
+#define PT_CERT_INSIDE 0      // walk certificate: U = B* without the filter when every member's box lies in B*
+#endif
 #ifndef PT_WALK_SKIP
 #define PT_WALK_SKIP 1        // fast-forward the grid_fast walk to the members' union box (walk_skip)
 #endif
@@ -716,6 +719,26 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
     }
     if (cnt == 0) PT_CERT_FAIL(0)
     if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) PT_CERT_FAIL(1)
+#if PT_CERT_INSIDE
+    // A member whose voxel box lies inside B* adds nothing to U (B* is part of U),
+    // so it needs no entry test.  When every member is such (one member; or the
+    // common pair of a slab's faces in the same voxels), U = B* and the filter below
+    // -- a grown-box entry per member -- is skipped.
+    auto inside_b = [&](const int4 e) {
+        return (e.z & 1023) >= blx && ((e.z >> 10) & 1023) >= bly && ((e.z >> 20) & 1023) >= blz &&
+               (e.w & 1023) <= bhx && ((e.w >> 10) & 1023) <= bhy && ((e.w >> 20) & 1023) <= bhz;
+    };
+    bool need = false;
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 e = get(h);
+        need = need | (!(__int_as_float(e.x) == tmin) & !inside_b(e));
+    }
+    if (!need) {
+        ulx = blx; uly = bly; ulz = blz; uhx = bhx; uhy = bhy; uhz = bhz;
+    } else
+#endif
     {
         // sB: exact-ray entry parameter (from pt) of B*.  The walk enters its first
         // voxel of B* at a computed parameter <= sB + errm (errm: the largest
@@ -750,7 +773,11 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
             if (CAP > 0 && h >= nh) break;
             const int4 e = get(h);
             bool in = true;
+#if PT_CERT_INSIDE
+            if (use && __int_as_float(e.x) != tmin && !inside_b(e)) {
+#else
             if (use && __int_as_float(e.x) != tmin) {
+#endif
                 float g = -3.0e38f, go = 3.0e38f;
 #pragma unroll
                 for (int a = 0; a < 3; a++) {
@@ -1038,10 +1065,56 @@ __device__ __forceinline__ Hit make_hit(const KParams& p, float gdist, int gmode
     return h;
 }
 
+// Hit record of the split trace -> shade path (p.hit4 / p.hitm, slot j).
+// PT_HIT_TRI = 0: (dist, world normal) + model, the normal computed by the trace.
+// PT_HIT_TRI = 1: (dist, triangle) + model; the shading pass fetches the triangle
+// normal and transforms it (make_hit's float operations, so the same values):
+// the latency-bound trace loses a dependent gather and the transform.
+#ifndef PT_HIT_TRI
+#define PT_HIT_TRI 1
+#endif
+__device__ __forceinline__ void put_hit(const KParams& p, int j, float gdist, int gmodel, int gtri,
+                                        const ModelRec* models) {
+    if (PT_HIT_TRI) {
+        const bool any = gdist < kFMax;
+        p.hit4[j] = make_float4(any ? gdist : kFMax, __int_as_float(gtri), 0.0f, 0.0f);
+        p.hitm[j] = any ? gmodel : -1;
+        return;
+    }
+    Hit h;
+    h.dist = kFMax; h.n = mk3(0, 0, 0); h.model = -1;
+    if (gdist < kFMax) {
+        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
+        h.dist = gdist;
+        h.model = gmodel;
+        h.n = normalize(xform_normal9(models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
+    }
+    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
+    p.hitm[j] = h.model;
+}
+__device__ __forceinline__ Hit get_hit(const KParams& p, int hj) {
+    const float4 hh = ld_ray<2>(p.hit4 + hj);
+    Hit h;
+    h.dist = hh.x;
+    h.model = p.hitm[hj];
+    if (PT_HIT_TRI) {
+        h.n = mk3(0, 0, 0);
+        if (h.model >= 0) {
+            const int tri = __float_as_int(hh.y);
+            const float4 tn = tri >= 0 ? p.tri_normal[tri] : make_float4(0, 0, 0, 0);
+            h.n = normalize(xform_normal9(p.models[h.model].nm, mk3(tn.x, tn.y, tn.z)));
+        }
+    } else {
+        h.n = mk3(hh.y, hh.z, hh.w);
+    }
+    return h;
+}
+
 template <int ACCEL, int STRIDE>
-__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs) {
-    float gdist = kFMax;
-    int gmodel = -1, gtri = -1;
+__device__ void intersect_scene_g(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs, float& gdist, int& gmodel,
+                                  int& gtri) {
+    gdist = kFMax;
+    gmodel = -1; gtri = -1;
     const f3 winv = node_inv(cull_inv(dir));
     const float dlen = sqrtf(dot(dir, dir));
     for (int im = 0; im < p.nmodels; im++) {
@@ -1061,6 +1134,13 @@ __device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, in
             if (gdist > dd) { gdist = dd; gmodel = im; gtri = best_tri; }
         }
     }
+}
+
+template <int ACCEL, int STRIDE>
+__device__ Hit intersect_scene(const KParams& p, f3 orig, f3 dir, int* stack, int4* hs) {
+    float gdist;
+    int gmodel, gtri;
+    intersect_scene_g<ACCEL, STRIDE>(p, orig, dir, stack, hs, gdist, gmodel, gtri);
     return make_hit(p, gdist, gmodel, gtri);
 }
 
@@ -1501,16 +1581,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             for (;;) {
                 im++;
                 if (im >= p.nmodels) {
-                    Hit h;
-                    h.dist = kFMax; h.n = mk3(0, 0, 0); h.model = -1;
-                    if (gdist < kFMax) {
-                        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
-                        h.dist = gdist;
-                        h.model = gmodel;
-                        h.n = normalize(xform_normal9(models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
-                    }
-                    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
-                    p.hitm[j] = h.model;
+                    put_hit(p, j, gdist, gmodel, gtri, models);
                     state = 0;
                     break;
                 }
@@ -1696,6 +1767,13 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_MINWAVES
 #define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
 #endif
+// Walk hand-on records reserved per wave in runs of PT_HANDON_CHUNK (one atomic per
+// run instead of one per hand-on batch); unused records of a run are marked
+// (state -1) and skipped by the tail.  0: one atomic per batch.
+#ifndef PT_HANDON_CHUNK
+#define PT_HANDON_CHUNK 0
+#endif
+constexpr int kHandonChunk = PT_HANDON_CHUNK;
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
@@ -1846,6 +1924,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
+    int w_next = 0, w_end = 0;                      // kHandonChunk: the wave's reserved walk hand-on records
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
@@ -1886,7 +1965,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     for (int q = 0; q < kGfHitCap; q++)
                         hs[q * BS] = make_int4(C[(kCX + 9 + kGfStack + 4 * q) * cs], C[(kCX + 10 + kGfStack + 4 * q) * cs],
                                                C[(kCX + 11 + kGfStack + 4 * q) * cs], C[(kCX + 12 + kGfStack + 4 * q) * cs]);
-                    if (state != 1) {                       // inside model im: its model-space ray, as selected
+                    if (state > 1) {                        // inside model im: its model-space ray, as selected
                         const ModelRec& M = models[im];
                         o = xform12(M.w2m, ow, 1.0f);
                         d = normalize(xform12(M.w2m, dw, 0.0f));
@@ -1894,6 +1973,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                         ninv = node_inv(inv);
                         set_qframe(M);
                     }
+                    if (kHandonChunk > 0 && state < 0) state = 0;   // an unused reserved record
                 } else {
                     state = 3;
                 }
@@ -1950,11 +2030,18 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
         }
         if (exhausted && state == 0) state = 3;
-        if (__ballot(state != 3) == 0) break;
+        // on the way out: the reserved run's unused records are marked, so the tail skips them
+        auto mark_holes = [&]() {
+            const int hole = w_next + lane;
+            if (kHandonChunk > 0 && !TAIL && hole < w_end && hole < p.cont_wcap)
+                cout[(size_t)kCState * p.cont_cap + (p.cont_cap - 1 - hole)] = -1;
+        };
+        if (__ballot(state != 3) == 0) { mark_holes(); break; }
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
         // the cap's kernel-argument load stays out of the loop's common path
         if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
             if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
+            mark_holes();
             break;
         }
         int phase = 15;
@@ -1990,16 +2077,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             for (;;) {
                 im++;
                 if (im >= p.nmodels) {
-                    Hit h;
-                    h.dist = kFMax; h.n = mk3(0, 0, 0); h.model = -1;
-                    if (gdist < kFMax) {
-                        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
-                        h.dist = gdist;
-                        h.model = gmodel;
-                        h.n = normalize(xform_normal9(models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
-                    }
-                    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
-                    p.hitm[j] = h.model;
+                    put_hit(p, j, gdist, gmodel, gtri, models);
                     state = 0;
                     break;
                 }
@@ -2276,8 +2354,26 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const int nbusy = __popcll(bm);
             const int leader = __ffsll((long long)bm) - 1;
             int base = 0;
-            if (lane == leader) base = atomicAdd(p.cont_count + (drain ? level : kDrainLevels + level), nbusy);
-            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
+            if (kHandonChunk > 0 && !drain) {
+                // walk hand-ons from the wave's reserved run of records; one atomic per chunk
+                if (w_end - w_next < nbusy) {
+                    // the run's rest cannot take them all: mark it unused (the tail skips such
+                    // records) and reserve a new run
+                    const int hole = w_next + lane;
+                    if (hole < w_end && hole < p.cont_wcap)
+                        cout[(size_t)kCState * p.cont_cap + (p.cont_cap - 1 - hole)] = -1;
+                    const int R = max(nbusy, kHandonChunk);
+                    if (lane == leader) base = atomicAdd(p.cont_count + kDrainLevels + level, R);
+                    w_next = __builtin_amdgcn_readlane(base, leader);
+                    w_end = w_next + R;
+                }
+                base = w_next;
+                w_next = __builtin_amdgcn_readfirstlane(w_next + nbusy);   // uniform: SGPRs
+                w_end = __builtin_amdgcn_readfirstlane(w_end);
+            } else {
+                if (lane == leader) base = atomicAdd(p.cont_count + (drain ? level : kDrainLevels + level), nbusy);
+                base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
+            }
             const int r = base + __popcll(bm & ((1ull << lane) - 1ull));
             if (!drain && mine && r >= p.cont_wcap) {  // no room left: the whole ray goes to k_trace_deferred
                 p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
@@ -2349,10 +2445,11 @@ __global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
         const int src = p.hit_order ? p.order[j].y : slot_source(p, j);
         const float4 a = p.ray[in_buf][0][kRS * src];
         const float4 b = p.ray[in_buf][1][kRS * src];
-        const Hit h = intersect_scene<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z),
-                                                           s_stack + threadIdx.x, s_hs + threadIdx.x);
-        p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
-        p.hitm[j] = h.model;
+        float gdist;
+        int gmodel, gtri;
+        intersect_scene_g<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), s_stack + threadIdx.x,
+                                               s_hs + threadIdx.x, gdist, gmodel, gtri);
+        put_hit(p, j, gdist, gmodel, gtri, p.models);
     }
 }
 
@@ -2413,10 +2510,7 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
             r.c = mk3(c.x, c.y, c.z);
             if (ACCEL == kAccelHitBuffer) {       // traced by k_trace_bvh / k_trace_gf
                 const int hj = p.hit_order ? p.slot_pos[j] : j;   // hit_order: records sit in claim order
-                const float4 hh = ld_ray<2>(p.hit4 + hj);
-                h.dist = hh.x;
-                h.n = mk3(hh.y, hh.z, hh.w);
-                h.model = p.hitm[hj];
+                h = get_hit(p, hj);
             } else {
                 h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
             }
