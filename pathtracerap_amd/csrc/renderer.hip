@@ -1767,13 +1767,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_MINWAVES
 #define PT_GF_MINWAVES 4      // waves per SIMD the register allocation must allow
 #endif
-// Walk hand-on records reserved per wave in runs of PT_HANDON_CHUNK (one atomic per
-// run instead of one per hand-on batch); unused records of a run are marked
-// (state -1) and skipped by the tail.  0: one atomic per batch.
-#ifndef PT_HANDON_CHUNK
-#define PT_HANDON_CHUNK 0
-#endif
-constexpr int kHandonChunk = PT_HANDON_CHUNK;
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
@@ -1924,7 +1917,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
-    int w_next = 0, w_end = 0;                      // kHandonChunk: the wave's reserved walk hand-on records
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
@@ -1973,7 +1965,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                         ninv = node_inv(inv);
                         set_qframe(M);
                     }
-                    if (kHandonChunk > 0 && state < 0) state = 0;   // an unused reserved record
                 } else {
                     state = 3;
                 }
@@ -2030,18 +2021,11 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
         }
         if (exhausted && state == 0) state = 3;
-        // on the way out: the reserved run's unused records are marked, so the tail skips them
-        auto mark_holes = [&]() {
-            const int hole = w_next + lane;
-            if (kHandonChunk > 0 && !TAIL && hole < w_end && hole < p.cont_wcap)
-                cout[(size_t)kCState * p.cont_cap + (p.cont_cap - 1 - hole)] = -1;
-        };
-        if (__ballot(state != 3) == 0) { mark_holes(); break; }
+        if (__ballot(state != 3) == 0) break;
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
         // the cap's kernel-argument load stays out of the loop's common path
         if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
             if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
-            mark_holes();
             break;
         }
         int phase = 15;
@@ -2354,26 +2338,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const int nbusy = __popcll(bm);
             const int leader = __ffsll((long long)bm) - 1;
             int base = 0;
-            if (kHandonChunk > 0 && !drain) {
-                // walk hand-ons from the wave's reserved run of records; one atomic per chunk
-                if (w_end - w_next < nbusy) {
-                    // the run's rest cannot take them all: mark it unused (the tail skips such
-                    // records) and reserve a new run
-                    const int hole = w_next + lane;
-                    if (hole < w_end && hole < p.cont_wcap)
-                        cout[(size_t)kCState * p.cont_cap + (p.cont_cap - 1 - hole)] = -1;
-                    const int R = max(nbusy, kHandonChunk);
-                    if (lane == leader) base = atomicAdd(p.cont_count + kDrainLevels + level, R);
-                    w_next = __builtin_amdgcn_readlane(base, leader);
-                    w_end = w_next + R;
-                }
-                base = w_next;
-                w_next = __builtin_amdgcn_readfirstlane(w_next + nbusy);   // uniform: SGPRs
-                w_end = __builtin_amdgcn_readfirstlane(w_end);
-            } else {
-                if (lane == leader) base = atomicAdd(p.cont_count + (drain ? level : kDrainLevels + level), nbusy);
-                base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
-            }
+            if (lane == leader) base = atomicAdd(p.cont_count + (drain ? level : kDrainLevels + level), nbusy);
+            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             const int r = base + __popcll(bm & ((1ull << lane) - 1ull));
             if (!drain && mine && r >= p.cont_wcap) {  // no room left: the whole ray goes to k_trace_deferred
                 p.defer_slots[atomicAdd(p.defer_count, 1)] = j;
