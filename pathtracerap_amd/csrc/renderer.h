@@ -81,6 +81,9 @@ struct KParams {
     int sort_mode;                      // key layout (k_sort_hist); 0 = no sort
     int hit_order;                      // 1: hit records at claim positions, slot_pos[j] = j's position (PT_HIT_ORDER)
     int* slot_pos;
+    float4* sray;                       // PT_SORT_COPY: rays in claim order, 2 float4 per position:
+                                        // (o.xyz, dense slot as int bits), (d.xyz, bounces); null: gather via order
+    int sort_copy;                      // 1: k_sort_scatter writes sray (PT_SORT_COPY)
     float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
     int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
     int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)

@@ -70,6 +70,10 @@ constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS)
 #define PT_SORT_BITS 12       // ray sort key bits (14: key 9, 15: key 10 -- finer cells, bigger LDS histograms)
 #endif
 constexpr int kSortBits = PT_SORT_BITS, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
+#ifndef PT_SORT_COPY
+#define PT_SORT_COPY 0        // default of the PT_SORT_COPY env switch (rays copied to their claim positions)
+#endif
+constexpr bool kSortCopyDefault = PT_SORT_COPY != 0;
 #ifndef PT_SORT_WG
 #define PT_SORT_WG 512
 #endif
@@ -1502,11 +1506,17 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 if (state == 0) {
                     j = base + __popcll(idle & ((1ull << lane) - 1ull));
                     if (j < n) {
-                        int src;
-                        if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
-                        else src = slot_source(p, j);
-                        const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
-                        const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
+                        float4 a, b;
+                        if (p.sray) {                   // the ray copied in claim order: one coalesced 32-B read
+                            a = ld_ray<1>(p.sray + 2 * j); b = ld_ray<1>(p.sray + 2 * j + 1);
+                            j = p.hit_order ? j : __float_as_int(a.w);
+                        } else {
+                            int src;
+                            if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
+                            else src = slot_source(p, j);
+                            a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
+                            b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
+                        }
                         ow = mk3(a.x, a.y, a.z);
                         dw = mk3(b.x, b.y, b.z);
                         winv = node_inv(cull_inv(dw));
@@ -2006,11 +2016,17 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (state == 0) {
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
-                    int src;
-                    if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
-                    else src = slot_source(p, j);
-                    const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
-                    const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
+                    float4 a, b;
+                    if (p.sray) {                   // the ray copied in claim order: one coalesced 32-B read
+                        a = ld_ray<1>(p.sray + 2 * j); b = ld_ray<1>(p.sray + 2 * j + 1);
+                        j = p.hit_order ? j : __float_as_int(a.w);
+                    } else {
+                        int src;
+                        if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
+                        else src = slot_source(p, j);
+                        a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
+                        b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
+                    }
                     ow = mk3(a.x, a.y, a.z);
                     dw = mk3(b.x, b.y, b.z);
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
@@ -2734,6 +2750,7 @@ __global__ __launch_bounds__(kSortWG) void k_sort_prefix(KParams p) {
 
 __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce) {
     __shared__ int s_h[kSortBins];                       // local counts, then this workgroup's base per key
+    const int in_buf = (bounce + 1) & 1;
     const int nprev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
     const int lim = ((nprev + p.chunk - 1) / p.chunk) * p.chunk;
     const int i0 = blockIdx.x * (kSortWG * kSortPer);
@@ -2766,6 +2783,13 @@ __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce)
         if (key[t] >= 0) {
             const int pos = s_h[key[t]] + rank[t];
             p.order[pos] = make_int2(jj[t], i0 + t * kSortWG + tid);
+            if (p.sray) {                                // PT_SORT_COPY: the ray itself, in claim order
+                const int i = i0 + t * kSortWG + tid;
+                const float4 a = ld_ray<4>(p.ray[in_buf][0] + kRS * i);
+                const float4 b = ld_ray<4>(p.ray[in_buf][1] + kRS * i);
+                p.sray[2 * pos] = make_float4(a.x, a.y, a.z, __int_as_float(jj[t]));
+                p.sray[2 * pos + 1] = b;
+            }
             if (p.hit_order) p.slot_pos[jj[t]] = pos;
         }
 }
@@ -2986,6 +3010,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         // shading pass finds slot j's record through slot_pos[j].  Results identical.
         const char* ho = std::getenv("PT_HIT_ORDER");
         kp.hit_order = kp.sort_mode && ho && std::atoi(ho) != 0;
+        // PT_SORT_COPY=1: the scatter copies each ray to its claim position, so a trace refill
+        // reads (ray, slot) in one coalesced load instead of the order entry and then the ray
+        const char* sc = std::getenv("PT_SORT_COPY");
+        kp.sort_copy = kp.sort_mode && (sc ? std::atoi(sc) != 0 : kSortCopyDefault);
         float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
         for (const ModelRec& m : scene.model_recs)
             for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], m.wbox[a]); hi[a] = std::max(hi[a], m.wbox[3 + a]); }
@@ -2995,7 +3023,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
             kp.sort_sc[a] = ext > 0.0f && ext < 1e30f ? 16.0f / ext : 0.0f;
         }
     }
-    kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr;
+    kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr; kp.sray = nullptr;
     kp.top_nodes = nullptr;
     kp.top_mesh = -1;
     kp.qnodes = nullptr;
@@ -3164,6 +3192,7 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
         PT_HIP(upload(allocs, &k.sort_key, nullptr, cap * sizeof(unsigned short), st));
         PT_HIP(upload(allocs, &k.sort_bins, nullptr, 2 * kSortBins * sizeof(int), st));
         PT_HIP(upload(allocs, &k.slot_pos, nullptr, (k.hit_order ? cap : 1) * sizeof(int), st));
+        if (k.sort_copy) PT_HIP(upload(allocs, &k.sray, nullptr, 2 * cap * sizeof(float4), st));
         PT_HIP(hipMemsetAsync(k.sort_bins, 0, 2 * kSortBins * sizeof(int), st));
     }
     const size_t hcap = split_trace ? cap : 1;

@@ -529,3 +529,25 @@ def test_hit_order_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch
         img, seg, oimg, oseg = _render_both(P, O, s, cfg)
         assert seg == oseg
         assert_bitexact(img, oimg, f"PT_HIT_ORDER accel={accel} pipes={pipes}")
+
+
+@pytest.mark.parametrize("accel", [1, 2])
+@pytest.mark.parametrize("pipes", [1, 4])
+@pytest.mark.parametrize("copy,hit_order", [("1", "0"), ("1", "1")])
+def test_sort_copy_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, pipes, copy, hit_order):
+    """PT_SORT_COPY=1: k_sort_scatter copies each ray, with its dense slot, to its
+    claim position, and the persistent traces' refills read it there (one
+    coalesced load instead of the claim-order entry and then the ray gather).
+    Only the claim path changes: images and segment counts stay the oracle's,
+    alone and with PT_HIT_ORDER."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_SORT_COPY", copy)
+    monkeypatch.setenv("PT_HIT_ORDER", hit_order)
+    for path in (synthetic.diffuse_scene(synth_dir, ntri=6000, seed=23, metallic=True), REF_SCENE):
+        s = P.Scene(path)
+        s.build()
+        cfg = P.RenderConfig(width=149, height=91, iterations=3, max_bounces=7, accel=accel, pipelines=pipes)
+        img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+        assert seg == oseg
+        assert_bitexact(img, oimg, f"PT_SORT_COPY={copy} PT_HIT_ORDER={hit_order} accel={accel} pipes={pipes}")
