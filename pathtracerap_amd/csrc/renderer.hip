@@ -74,6 +74,14 @@ constexpr int kSortBits = PT_SORT_BITS, kSortBins = 1 << kSortBits;   // ray sor
 #define PT_SORT_COPY 0        // default of the PT_SORT_COPY env switch (rays copied to their claim positions)
 #endif
 constexpr bool kSortCopyDefault = PT_SORT_COPY != 0;
+// PT_LATE_RAY: k_trace_gf's refill claims and reads the claim-order entry as before, but
+// the ray gather of the refilled lanes (state 8) is issued inside the next node step,
+// right after that step's node loads: vmcnt retires in issue order, so the node step
+// waits only for its own loads and the gather overlaps its arithmetic.  Any other
+// phase gathers at once, as without the option.
+#ifndef PT_LATE_RAY
+#define PT_LATE_RAY 0
+#endif
 #ifndef PT_SORT_WG
 #define PT_SORT_WG 512
 #endif
@@ -1927,6 +1935,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
+    constexpr bool late = PT_LATE_RAY && !TAIL && !(F & 4) && !kGfQ && kGfTop == 0;
+    bool pend8 = false;                             // late (uniform): lanes in state 8 wait for their ray gather
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
@@ -2016,7 +2026,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (state == 0) {
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
-                    float4 a, b;
+                    float4 a = make_float4(0, 0, 0, 0), b = a;
                     if (p.sray) {                   // the ray copied in claim order: one coalesced 32-B read
                         a = ld_ray<1>(p.sray + 2 * j); b = ld_ray<1>(p.sray + 2 * j + 1);
                         j = p.hit_order ? j : __float_as_int(a.w);
@@ -2024,18 +2034,27 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                         int src;
                         if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
                         else src = slot_source(p, j);
-                        a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
-                        b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
+                        if (late) {
+                            cur = src;              // the gather waits for the next node step (PT_LATE_RAY)
+                        } else {
+                            a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
+                            b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
+                        }
                     }
-                    ow = mk3(a.x, a.y, a.z);
-                    dw = mk3(b.x, b.y, b.z);
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                    state = 1;
+                    if (late && !p.sray) {
+                        state = 8;
+                    } else {
+                        ow = mk3(a.x, a.y, a.z);
+                        dw = mk3(b.x, b.y, b.z);
+                        state = 1;
+                    }
                 } else {
                     state = 3;
                 }
             }
         }
+        if (late) pend8 = __ballot(state == 8) != 0;
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
@@ -2056,6 +2075,16 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
+        if (late && pend8 && phase != 2) {            // no node step this iteration: gather now
+            if (state == 8) {
+                const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * cur);
+                const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * cur);
+                ow = mk3(a.x, a.y, a.z);
+                dw = mk3(b.x, b.y, b.z);
+                state = 1;
+            }
+            pend8 = false;
+        }
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
             {
@@ -2192,8 +2221,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 state = (tonext | pop) ? 2 : state;
                 sp -= pop ? 1 : 0;
             }
-        } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
+        } else if ((phase & 2) && (state == 2 || (late && pend8 && state == 8))) {   // one node of the collection (window t_min + win)
             const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+            const bool nd = !late || state == 2;        // late: state-8 lanes only gather their ray here
+            const int ncur = nd ? cur : 0;
             float4 q0, q1, q2, q3;
             if (kGfQ) {
                 // 16-bit planes: child 0 lo.xyz hi.xyz, child 1 lo.xyz hi.xyz; links in w0/w1 of
@@ -2231,11 +2262,19 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 q0 = make_float4(a0.x, a0.y, a0.z, a0.w); q1 = make_float4(a1.x, a1.y, a1.z, a1.w);
                 q2 = make_float4(a2.x, a2.y, a2.z, a2.w); q3 = make_float4(a3.x, a3.y, a3.z, a3.w);
             } else {
-                q0 = nodes[4 * cur + 0];
-                q1 = nodes[4 * cur + 1];
-                q2 = nodes[4 * cur + 2];
-                q3 = nodes[4 * cur + 3];
+                q0 = nodes[4 * ncur + 0];
+                q1 = nodes[4 * ncur + 1];
+                q2 = nodes[4 * ncur + 2];
+                q3 = nodes[4 * ncur + 3];
             }
+            if (late && !nd) {                          // the refilled lanes' gather, issued after the node loads
+                const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * cur);
+                const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * cur);
+                ow = mk3(a.x, a.y, a.z);
+                dw = mk3(b.x, b.y, b.z);
+                state = 1;
+            }
+            if (nd) {
             const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
             const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
             const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
@@ -2276,7 +2315,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
             lf_next = leaf ? next : lf_next;
             state = leaf ? 4 : state;
+            }
         }
+        if (late) pend8 = false;
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
         if (collected) {
             if (nh > 0) {
