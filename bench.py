@@ -12,14 +12,20 @@ displaced torus in an open-front room with emissive panels), 1280x1024,
 8 bounces.  One step = one sample per pixel = one full pass of the bounce
 loop (camera rays from the primary-hit cache, intersect, scatter, compact,
 accumulate) over the whole frame; the scene, ray pools and accumulator are
-resident in HBM before the timed region starts.  ``targets`` times two more
+resident in HBM before the timed region starts.  ``targets`` times more
 workloads the same way: north_star's target (the 1M-triangle diffuse OBJ at
-1280x1024) and configs[2] (the README render's own scene, Scene.cpp:3-224,
-at 2800x2240).
+1280x1024), configs[2] (the README render's own scene, Scene.cpp:3-224, at
+2800x2240) and configs[4] (the 10M-triangle scene, 16 bounces).  Each
+workload also renders its configuration's own sample count once (``full_run``:
+256 spp for configs[1], 1024 for the target and configs[2], 4096 for
+configs[4]; the reference's ITER, Config.h:19), timed the same way.
 
-Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): samples shard
-across ranks (rank r renders iterations [r*K, (r+1)*K)), then one RCCL
-all-reduce sums the float3 accumulator; weak scaling.
+Multi-GPU: ``--gpus N`` with N > 1 starts N ranks itself (one process per GPU,
+MASTER_ADDR 127.0.0.1) unless a launcher already set WORLD_SIZE
+(``torchrun --nproc-per-node N bench.py --gpus N``); either way the world size
+must equal N.  Samples shard across ranks (rank r renders iterations
+[r*K, (r+1)*K)), then one RCCL all-reduce sums the float3 accumulator; weak
+scaling.
 
 Prints ONE JSON line (rank 0).  ``value`` = ray segments shaded per second
 over all ranks (a segment = one live ray in one bounce, the primary rays whose
@@ -32,6 +38,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -45,11 +54,15 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 # 2 cycles (32 lanes/cycle, MI355X_MICROARCH.md:54 and its constants table, v_fma_f32
 # "2 cyc (SIMD-32)"), 2.4 GHz
 VALU_PEAK_G = 256 * 4 * 2.4 / 2
+# samples per pixel each BASELINE.json configuration asks for (full_run)
+SPP = {"configs1": 256, "target_1m": 1024, "configs2": 1024, "configs4": 4096}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="GPUs (ranks); 0: WORLD_SIZE when a launcher set it, else 1.  N > 1 without a launcher: "
+                         "bench.py starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--accel", choices=["bvh", "grid", "grid_fast"], default="grid_fast",
@@ -63,23 +76,93 @@ def parse():
     ap.add_argument("--metallic", action="store_true")
     ap.add_argument("--scene", default="", help="a scene file instead of the synthetic OBJ scene (e.g. "
                                                 "scenes/reference_scene.txt); its RENDER block's bounces apply")
-    ap.add_argument("--targets", default="target_1m,configs2",
+    ap.add_argument("--targets", default="target_1m,configs2,configs4",
                     help="extra workloads timed after the main line ('' to skip): target_1m = north_star's "
-                         "1M-triangle scene at 1280x1024; configs2 = the README scene at 2800x2240")
+                         "1M-triangle scene at 1280x1024; configs2 = the README scene at 2800x2240; configs4 = "
+                         "the 10M-triangle scene at 1280x1024, 16 bounces")
     ap.add_argument("--target-steps", type=int, default=16)
+    ap.add_argument("--no-full-runs", action="store_true",
+                    help="skip the full-spp renders (256 / 1024 / 1024 / 4096 spp) of each workload")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events (neither in the timed "
-                                                              "region nor the one-pipeline pass)")
+    ap.add_argument("--no-profile", action="store_true", help="no one-pipeline HIP-event pass (roofline)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank path with several ranks on one GPU)")
     ap.add_argument("--pipelines", type=int, default=16,
                     help="iterations in flight on their own HIP streams (0: the library default, 16)")
     ap.add_argument("--hw-queues", type=int, default=16,
-                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4; the library also defaults it "
-                         "to 16): one hardware queue per pipeline stream (max 32)")
-    return ap.parse_args()
+                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4): one hardware queue per "
+                         "pipeline stream (max 32)")
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(n, argv):
+    """--gpus N without a launcher: start ranks 0..N-1 of this script as child
+    processes (nothing here has touched the GPU: the parent only waits), rank 0's
+    stdout is the JSON line.  If a rank fails, the others are stopped (they would
+    wait in a collective forever) and the failing exit code is returned."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+                deadline = time.time() + 15
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        try:
+                            os.killpg(q.pid, signal.SIGKILL)
+                        except ProcessLookupError:
+                            pass
+                        q.wait()
+                live = []
+                break
+        time.sleep(0.1)
+    return rc
+
+
+def host_cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota
+    and by the pool's per-GPU share (OMP_NUM_THREADS, set on the GPU box) when
+    those exist.  Returns (threads, description)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n, why = aff, [f"affinity mask {aff} CPUs"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            why.append(f"cgroup quota {q} CPUs")
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        why.append(f"OMP_NUM_THREADS {omp} (the pool's CPU share per GPU)")
+        n = min(n, int(omp))
+    return max(1, n), ", ".join(why)
 
 
 def cpu_baseline(scene_path, bounces, width, height, target_s):
@@ -91,7 +174,7 @@ def cpu_baseline(scene_path, bounces, width, height, target_s):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import flat_from_export
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1))
+    threads, share = host_cpu_share()
     s = P.Scene(scene_path)
     s.build()
     flat = flat_from_export(s.export())
@@ -112,19 +195,17 @@ def cpu_baseline(scene_path, bounces, width, height, target_s):
         f = max(1.0, frames) ** 0.5
         w, h = min(width, int(w * f)), min(height, int(h * f))
     seg, dt = run(w, h, iters)
-    return {"value": seg / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": seg / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port", "cpu_share": share,
             "sample": f"oracle/ptoracle.c (C port of the reference renderLoop, uniform-grid accel as in "
-                      f"the reference) on the same scene/camera at {w}x{h}, {iters} spp, {bounces} bounces: "
-                      f"{seg} segments in {dt:.2f}s on {threads} thread(s)"}
+                      f"the reference, OpenMP over rays) on the same scene/camera at {w}x{h}, {iters} spp, "
+                      f"{bounces} bounces: {seg} segments in {dt:.2f}s on {threads} thread(s) ({share})"}
 
 
 def workload_name(args):
     """Label of the BASELINE.json configuration this run measures."""
     if args.scene:
         return f"scene file {os.path.relpath(args.scene, ROOT)}, {args.width}x{args.height}, {args.bounces} bounces"
-    default = (args.ntri == 100_000 and args.width == 1280 and args.height == 1024 and args.bounces == 8
-               and not args.metallic)
-    if default:
+    if is_default_workload(args):
         return "configs[1]: diffuse-only synthetic OBJ (~100k tris), 1280x1024, 8 bounces"
     kind = "metallic+diffuse" if args.metallic else "diffuse-only"
     tag = ""
@@ -133,6 +214,11 @@ def workload_name(args):
     elif not args.metallic and args.ntri >= 500_000:
         tag = "north_star target shape: "
     return f"{tag}{kind} synthetic OBJ (~{args.ntri} tris), {args.width}x{args.height}, {args.bounces} bounces"
+
+
+def is_default_workload(args):
+    return (not args.scene and args.ntri == 100_000 and args.width == 1280 and args.height == 1024
+            and args.bounces == 8 and not args.metallic)
 
 
 def load_pmc(kernel, workload_key):
@@ -178,13 +264,17 @@ class Ctx:
         return [float(x) for x in t.cpu()]
 
 
-def timed_run(P, ctx, scene, cfg, K, W, iter_base, events, reduce_image):
+def timed_run(P, ctx, scene, cfg, K, W, iter_base, reduce_image, full_spp=0):
     """Warm up, then time exactly K iterations (this rank's [rank*K, (rank+1)*K))
     between barrier + synchronize pairs; the accumulator all-reduce (RCCL) is
-    inside the timed region.  ``events``: per-kernel HIP events on the pipeline
-    streams during the timed region (renderer profiling mode).  Returns the
-    max-over-ranks time, the all-rank segment total and the renderer's stats."""
-    torch, dev, rank = ctx.torch, ctx.dev, ctx.rank
+    inside the timed region.  No profiling events in the timed region.  With
+    ``full_spp`` the same renderer then renders iterations [0, full_spp) sharded
+    over the ranks (the configuration's own sample count), timed the same way.
+    Trace faults (waves that hit the iteration cap) of the warmup and of both
+    timed regions make the run invalid.  Returns the max-over-ranks times, the
+    all-rank segment totals and the per-bounce counts of rank 0's K steps."""
+    from pathtracerap_amd.dist import shard_iterations
+    torch, dev, rank, world = ctx.torch, ctx.dev, ctx.rank, ctx.world
     image = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device=dev)
     r = P.Renderer(cfg)
     r.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -193,42 +283,55 @@ def timed_run(P, ctx, scene, cfg, K, W, iter_base, events, reduce_image):
     # warmup: builds the primary-hit cache, warms caches/clocks; distinct iteration ids
     r.renderLoop(first_iter=iter_base + rank * max(W, 1), n_iters=W, sync=False)
     torch.cuda.synchronize(dev)
-    if reduce_image and ctx.world > 1:
+    faults = r.trace_faults()          # clearImage resets the counter: read the warmup's first
+    if reduce_image and world > 1:
         # warm the accumulator-sized all-reduce: one-time RCCL setup is paid here
         ctx.dist.all_reduce(image, op=ctx.dist.ReduceOp.SUM)
         torch.cuda.synchronize(dev)
-    r.clearImage()
-    seg0 = r.segments()
-    pb0 = r.segments_per_bounce()
-    if events:
-        r.kernel_stats()                   # reset
-        r.set_profiling(2)                 # event pairs around pipeline 0's trace phases only
-    ctx.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    r.renderLoop(first_iter=rank * K, n_iters=K, sync=False)
-    if reduce_image and ctx.world > 1:
-        ctx.dist.all_reduce(image, op=ctx.dist.ReduceOp.SUM)      # RCCL over xGMI
-    torch.cuda.synchronize(dev)
-    ctx.barrier()
-    t1 = time.perf_counter()
-    stats = r.kernel_stats() if events else None
+
+    def region(first, n):
+        r.clearImage()
+        ctx.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r.renderLoop(first_iter=first, n_iters=n, sync=False)
+        if reduce_image and world > 1:
+            ctx.dist.all_reduce(image, op=ctx.dist.ReduceOp.SUM)      # RCCL over xGMI
+        torch.cuda.synchronize(dev)
+        ctx.barrier()
+        return time.perf_counter() - t0
+
+    seg0, pb0 = r.segments(), r.segments_per_bounce()
+    elapsed = region(rank * K, K)
+    faults += r.trace_faults()
     seg = r.segments() - seg0
     per_bounce = [a - b for a, b in zip(r.segments_per_bounce(), pb0)]
     while per_bounce and per_bounce[-1] == 0:
         per_bounce.pop()
-    faults = r.trace_faults()
     img_ok = bool(torch.isfinite(image).all().item())
+    full = None
+    if full_spp > 0:
+        first, n = shard_iterations(full_spp, rank, world)
+        segf0, pbf0 = r.segments(), r.segments_per_bounce(1)[0]
+        el_full = region(first, n)
+        faults += r.trace_faults()
+        full = [el_full, float(r.segments() - segf0), float(r.segments_per_bounce(1)[0] - pbf0),
+                float(torch.isfinite(image).all().item())]
     pipes = r.pipelines()
     r.free()
     # every rank learns of a fault on any rank and stops together (no rank left in a collective)
-    fmax, elapsed = ctx.reduce([float(faults), t1 - t0], "max")
+    fmax, el_max = ctx.reduce([float(faults), elapsed], "max")
     seg_total, seg0_total = ctx.reduce([float(seg), float(per_bounce[0] if per_bounce else 0)], "sum")
     if fmax > 0:
         raise SystemExit(f"bench: persistent-trace wave(s) hit the iteration cap on some rank "
                          f"(max {int(fmax)}); result invalid")
-    return dict(elapsed=elapsed, seg=seg_total, seg_primary=seg0_total, per_bounce=per_bounce, stats=stats,
-                img_ok=img_ok, pipes=pipes, faults=int(fmax))
+    res = dict(elapsed=el_max, seg=seg_total, seg_primary=seg0_total, per_bounce=per_bounce, img_ok=img_ok,
+               pipes=pipes, faults=int(fmax))
+    if full is not None:
+        fel, = ctx.reduce([full[0]], "max")
+        fseg, fseg0, fok = ctx.reduce(full[1:], "sum")
+        res["full"] = dict(spp=full_spp, elapsed=fel, seg=fseg, seg_primary=fseg0, img_ok=fok == world)
+    return res
 
 
 def rates(res, K, npix, world):
@@ -238,21 +341,62 @@ def rates(res, K, npix, world):
             "ms_per_step": round(e / K * 1e3, 3), "samples_per_sec": round(world * K * npix / e, 1)}
 
 
+def full_rates(res, npix):
+    """The full-spp render: spp iterations over all ranks in `elapsed` seconds."""
+    f = res.get("full")
+    if not f:
+        return None
+    e = f["elapsed"]
+    return {"spp": f["spp"], "seconds": round(e, 4), "value": round(f["seg"] / e / 1e6, 3), "unit": "Mrays/s",
+            "traced_mrays_per_sec": round((f["seg"] - f["seg_primary"]) / e / 1e6, 3),
+            "samples_per_sec": round(f["spp"] * npix / e, 1), "segments": int(f["seg"]), "image_finite": f["img_ok"]}
+
+
 def trace_bytes_per_step(per_bounce, K):
     """Algorithmic HBM bytes of the persistent trace per step: every segment entering
     bounce b >= 1 reads its ray (o, d: 32 B) and writes its 20-B hit record."""
     return 52.0 * sum(per_bounce[1:]) / K
 
 
+def one_pipeline_pass(P, torch, dev, scene, cfg, K, W):
+    """Per-kernel HIP-event durations of ONE pipeline (no overlapping launches):
+    the same K iterations as the timed region (same ids => the same per-bounce
+    ray counts), events recorded on the pipeline's stream around every kernel
+    group (renderer profiling level 1)."""
+    cfg_p = P.RenderConfig(**{**cfg.__dict__, "pipelines": 1})
+    image = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device=dev)
+    rp = P.Renderer(cfg_p)
+    rp.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rp.bind_image(image.data_ptr(), keepalive=image)
+    rp.allocateOnGPU(scene)
+    rp.renderLoop(first_iter=1_000_000, n_iters=W, sync=False)
+    torch.cuda.synchronize(dev)
+    rp.kernel_stats()          # reset
+    rp.set_profiling(1)
+    rp.renderLoop(first_iter=0, n_iters=K, sync=True)
+    st = rp.kernel_stats()
+    rp.free()
+    return st
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the ranks here, before anything touches the GPU
+        if args.hw_queues > 0:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    if args.gpus and args.gpus != world:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.hw_queues > 0:     # read once by the HIP runtime at initialisation: set before torch touches it
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
+    import pathtracerap_amd as P            # loads the library before HIP starts (its load-time checks)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     # one rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on a 1-GPU
     # box) ranks share devices round-robin
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -266,7 +410,6 @@ def main():
     torch.cuda.set_device(dev)
     ctx = Ctx(torch, dist, dev, rank, world)
 
-    import pathtracerap_amd as P
     from pathtracerap_amd import synthetic
 
     accels = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}
@@ -289,31 +432,18 @@ def main():
     ntri = scene.counts()["nt"]
     npix = cfg.width * cfg.height
     K, W = args.steps, args.warmup
-    events = not args.no_profile
+    full_main = 0 if args.no_full_runs or not is_default_workload(args) else SPP["configs1"]
 
-    main_res = timed_run(P, ctx, scene, cfg, K, W, 1_000_000, events, reduce_image=True)
+    main_res = timed_run(P, ctx, scene, cfg, K, W, 1_000_000, reduce_image=True, full_spp=full_main)
     per_bounce = main_res["per_bounce"]
     workload_key = f"{args.accel}_{args.ntri}_{args.width}x{args.height}_b{args.bounces}" + \
         ("_metal" if args.metallic else "")
 
-    # Per-kernel durations of ONE pipeline, for comparison with the timed run's
-    # overlapping launches: a separate pass of the same K iterations (same ids =>
-    # the same per-bounce ray counts), rank 0 only while the others wait.
+    # Per-kernel durations of ONE pipeline (rank 0 while the others wait): the
+    # dominant kernel's launches without the overlap of the 16 iterations in flight
     stats1 = None
-    if events and rank == 0:
-        cfg_p = P.RenderConfig(**{**cfg.__dict__, "pipelines": 1})
-        image = torch.zeros(npix * 3, dtype=torch.float32, device=dev)
-        rp = P.Renderer(cfg_p)
-        rp.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        rp.bind_image(image.data_ptr(), keepalive=image)
-        rp.allocateOnGPU(scene)
-        rp.renderLoop(first_iter=1_000_000, n_iters=W, sync=False)
-        torch.cuda.synchronize(dev)
-        rp.kernel_stats()          # reset
-        rp.set_profiling(True)
-        rp.renderLoop(first_iter=rank * K, n_iters=K, sync=True)
-        stats1 = rp.kernel_stats()
-        rp.free()
+    if not args.no_profile and rank == 0:
+        stats1 = one_pipeline_pass(P, torch, dev, scene, cfg, K, W)
     ctx.barrier()
 
     alt = None
@@ -322,7 +452,7 @@ def main():
         cfg2 = P.RenderConfig(**{**cfg.__dict__, "accel": acc2})
         if acc2 != P.ACCEL_GRID and accel == P.ACCEL_GRID:
             scene.build(grid=cfg.grid, bvh=True)
-        ra = timed_run(P, ctx, scene, cfg2, K, W, 2_000_000, False, reduce_image=False)
+        ra = timed_run(P, ctx, scene, cfg2, K, W, 2_000_000, reduce_image=False)
         alt = {"accel": args.alt_accel, **rates(ra, K, npix, world),
                "semantics": "exact closest hit (statistically equivalent image, not per-pixel identical)"
                if args.alt_accel == "bvh" else "reference grid (bit-identical)"}
@@ -330,94 +460,98 @@ def main():
     targets = {}
     tk = max(1, min(K, args.target_steps))
     for name in [t for t in args.targets.split(",") if t]:
+        t_build = time.perf_counter()
         if name == "target_1m":
             path = synthetic.diffuse_scene(tmp, ntri=1_000_000, accel=args.accel)
             st = P.Scene(path)
             ct = st.apply_settings(P.RenderConfig())
-            label = ("north_star target: 1M-triangle diffuse synthetic OBJ, 1280x1024, 8 bounces "
-                     "(north_star asks 1024 spp: per-step rate)")
+            label = "north_star target: 1M-triangle diffuse synthetic OBJ, 1280x1024, 8 bounces"
         elif name == "configs2":
             st = P.Scene(os.path.join(ROOT, "scenes", "reference_scene.txt"))
             ct = st.apply_settings(P.RenderConfig())
             ct.width, ct.height = 2800, 2240
             label = ("configs[2]: the README render's scene (Scene.cpp:3-224: metal, coat, diffuse, emissive "
-                     "models), 2800x2240, the reference's 5 bounces (configs[2] asks 1024 spp: per-step rate)")
+                     "models), 2800x2240, the reference's 5 bounces")
+        elif name == "configs4":
+            # built in memory (addMesh / addModel): the 10M-triangle OBJ text would take
+            # about a minute to write and parse; same layout as diffuse_scene
+            st = None
+            ct = P.RenderConfig(width=1280, height=1024, max_bounces=16)
+            label = ("configs[4]: synthetic 10M-triangle diffuse scene (displaced torus in the room, deep BLAS), "
+                     "1280x1024, 16 bounces")
         else:
             raise SystemExit(f"bench: unknown target {name}")
         ct.accel = accel
         if args.pipelines > 0:
             ct.pipelines = args.pipelines
-        st.build(grid=ct.grid, bvh=accel != P.ACCEL_GRID)
-        rt = timed_run(P, ctx, st, ct, tk, min(W, 2), 3_000_000, False, reduce_image=True)
+        if st is None:
+            st = synthetic.build_scene(P, 10_000_000, grid=ct.grid, bvh=accel != P.ACCEL_GRID)
+        else:
+            st.build(grid=ct.grid, bvh=accel != P.ACCEL_GRID)
+        t_build = time.perf_counter() - t_build
+        spp = 0 if args.no_full_runs else SPP[name]
+        rt = timed_run(P, ctx, st, ct, tk, min(W, 2), 3_000_000, reduce_image=True, full_spp=spp)
+        tnpix = ct.width * ct.height
         targets[name] = {"workload": label, "triangles": st.counts()["nt"], "width": ct.width,
-                         "height": ct.height, "bounces": ct.max_bounces, "steps": tk, **rates(rt, tk, ct.width * ct.height, world),
-                         "segments": int(rt["seg"]), "image_finite": rt["img_ok"], "trace_faults": rt["faults"]}
+                         "height": ct.height, "bounces": ct.max_bounces, "steps": tk,
+                         **rates(rt, tk, tnpix, world), "segments": int(rt["seg"]), "image_finite": rt["img_ok"],
+                         "trace_faults": rt["faults"], "host_scene_build_s": round(t_build, 2),
+                         "full_run": full_rates(rt, tnpix)}
         del st
 
     if rank == 0:
         r_main = rates(main_res, K, npix, world)
         roof = None
-        stats = main_res["stats"]
-        if stats and stats.get("trace_launches", 0) > 0:
+        kname = "k_trace_bvh" if args.accel == "bvh" else "k_trace_gf"
+        tb_step = trace_bytes_per_step(per_bounce, K)
+        phases = max(1, len(per_bounce) - 1)                 # trace phases per step
+        b_launch = tb_step / phases                          # algorithmic bytes per launch (one bounce's trace)
+        job = tb_step / (main_res["elapsed"] / K) / 1e9      # per GPU: each rank runs K steps
+        per_step = {"achieved": round(job, 2), "frac": round(job / HBM_PEAK_GBS, 5),
+                    "algorithmic_bytes_per_step": round(tb_step), "ms_per_step": r_main["ms_per_step"],
+                    "note": "whole-job rate: algorithmic trace bytes per step / ms_per_step (16 iterations in "
+                            "flight share the step's wall time)"}
+        if stats1 and stats1.get("trace_launches", 0) > 0 and args.accel != "grid":
             # Dominant kernel: the persistent trace of bounces >= 1 (k_trace_gf / k_trace_bvh).
             # Algorithmic bytes per segment entering bounce b >= 1: 32 B ray read (o, d) + 20 B
-            # hit record write.  `achieved` = those bytes per step / ms_per_step: the launches of
-            # the 16 iterations in flight overlap, so the step's wall time is the time the
-            # kernel's work takes (a slight under-estimate: the other kernels share that time).
-            kname = "k_trace_bvh" if args.accel == "bvh" else "k_trace_gf"
-            tb_step = trace_bytes_per_step(per_bounce, K)
-            phases = max(1, len(per_bounce) - 1)                 # trace phases per step
-            job = tb_step / (main_res["elapsed"] / K) / 1e9      # per GPU: each rank runs K steps
-            # one "launch" = one bounce's trace phase (main launch + tail launches +
-            # k_trace_deferred), timed by an event pair on pipeline 0's stream in the timed region
-            launches = stats["trace_launches"]
-            kms = stats["trace_ms"] / launches
-            b_launch = tb_step / phases
-            a_launch = b_launch / (kms / 1e3) / 1e9
-            tr = load_pmc(kname, workload_key)                   # HBM bytes per launch, one pipeline
-            roof = {"bound": "hbm", "achieved": round(job, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(job / HBM_PEAK_GBS, 5),
-                    "traffic": None if tr is None else round(tr * phases),
-                    "kernel": kname, "basis": "per step: algorithmic trace bytes per step / ms_per_step "
-                                              "(traffic: PMC HBM bytes per launch x trace phases per step)",
-                    "algorithmic_bytes_per_step": round(tb_step), "ms_per_step": r_main["ms_per_step"],
-                    "trace_phases_per_step": phases, "traffic_per_launch": None if tr is None else round(tr),
-                    "per_launch": {
-                        "avg_launch_ms": round(kms, 4), "algorithmic_bytes_per_launch": round(b_launch),
-                        "achieved": round(a_launch, 2), "frac": round(a_launch / HBM_PEAK_GBS, 5),
-                        "launches_timed": launches, "pipelines": main_res["pipes"],
-                        "measured": "HIP event pair around each of pipeline 0's trace phases inside the timed "
-                                    "region: from the phase's turn on its stream to its last launch's end, so it "
-                                    "includes waiting for CU slots the other pipelines' kernels hold (rocprofv3 "
-                                    "times execution only: profiles/r03/kernel_stats_grid_fast_16p.csv)",
-                        "why_launches_exceed_step": (
-                            f"{phases} trace phases per step x {kms:.3f} ms = {phases * kms:.2f} ms of launch "
-                            f"time per step against {r_main['ms_per_step']:.3f} ms per step: "
-                            f"{main_res['pipes']} iterations are in flight, so about "
-                            f"{phases * kms / r_main['ms_per_step']:.1f} trace phases run at once")}}
-            if stats1 and stats1.get("trace_launches", 0) > 0:
-                l1 = stats1["trace_launches"]
-                k1 = stats1["trace_ms"] / l1
-                a1 = b_launch / (k1 / 1e3) / 1e9
-                roof["single_pipeline"] = {"avg_launch_ms": round(k1, 4), "achieved": round(a1, 2),
-                                           "frac": round(a1 / HBM_PEAK_GBS, 5), "launches": l1,
-                                           "sort_avg_ms": round(stats1["sort_ms"] / max(stats1["sort_launches"], 1), 4),
-                                           "shade_avg_ms": round(stats1["bounce_ms"] / max(stats1["bounce_launches"], 1), 4),
-                                           "scan_avg_ms": round(stats1["scan_ms"] / max(stats1["scan_launches"], 1), 4),
-                                           "measured": "HIP events, a separate pass of the same iterations with one "
-                                                       "pipeline (no overlap), rank 0"}
-        # Issue roofline: the traces are bound by instruction issue and dependent-load
-        # latency, not by HBM bytes, so the VALU issue rate against the SIMDs' peak is
-        # the informative fraction -- for the whole job (all kernels of a step, with the
-        # pipelines overlapping) and for the dominant kernel's single-pipeline launches.
+            # hit record write; one "launch" = one bounce's trace phase, timed by a HIP event
+            # pair on the stream it is launched on, with one pipeline (no overlap).
+            l1 = stats1["trace_launches"]
+            k1 = stats1["trace_ms"] / l1
+            a1 = b_launch / (k1 / 1e3) / 1e9
+            tr = load_pmc(kname, workload_key)               # PMC HBM bytes per launch, one pipeline
+            roof = {"bound": "hbm", "achieved": round(a1, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(a1 / HBM_PEAK_GBS, 5), "traffic": None if tr is None else round(tr),
+                    "kernel": kname,
+                    "basis": "per launch: algorithmic bytes of one bounce's trace (52 B x segments entering "
+                             "the bounce) / its average duration, HIP events on the launch stream, one "
+                             "pipeline (rocprofv3: profiles/r04/kernel_stats_*_1p.csv); traffic = PMC HBM bytes "
+                             "per launch of the same command (profiles/pmc_latest.json)",
+                    "algorithmic_bytes_per_launch": round(b_launch), "avg_launch_ms": round(k1, 4),
+                    "launches": l1, "trace_phases_per_step": phases, "per_step": per_step,
+                    "sort_avg_ms": round(stats1["sort_ms"] / max(stats1["sort_launches"], 1), 4),
+                    "shade_avg_ms": round(stats1["bounce_ms"] / max(stats1["bounce_launches"], 1), 4),
+                    "scan_avg_ms": round(stats1["scan_ms"] / max(stats1["scan_launches"], 1), 4)}
+            sq1 = load_sq(workload_key, "_sq_p1")
+            kv = (sq1 or {}).get("kernels", {}).get(kname)
+            if kv:
+                g = kv["valu_insts_per_launch"] / (k1 / 1e3) / 1e9
+                roof["issue"] = {"bound": "valu", "unit": "G wave-instr/s", "peak": VALU_PEAK_G,
+                                 "valu_insts_per_launch": round(kv["valu_insts_per_launch"]),
+                                 "achieved": round(g, 1), "frac": round(g / VALU_PEAK_G, 4),
+                                 "source": "rocprofv3 SQ_INSTS_VALU pass, one pipeline (profiles/pmc_latest.json) "
+                                           "/ avg_launch_ms"}
+        # Issue roofline of the whole job: the traces are bound by instruction issue and
+        # dependent-load latency, not by HBM bytes, so the VALU issue rate (all kernels of
+        # a step, the pipelines overlapping) against the SIMDs' peak is reported beside it.
         issue = None
         sq = load_sq(workload_key)
         if sq:
             v_step = sq["valu_insts_per_iteration"]
-            job = v_step * K / main_res["elapsed"] / 1e9      # per GPU: each rank runs K steps in `elapsed`
+            g = v_step * K / main_res["elapsed"] / 1e9      # per GPU: each rank runs K steps in `elapsed`
             issue = {"bound": "valu", "unit": "G wave-instr/s", "peak": VALU_PEAK_G,
-                     "job": {"valu_insts_per_step": round(v_step), "achieved": round(job, 1),
-                             "frac": round(job / VALU_PEAK_G, 4),
+                     "job": {"valu_insts_per_step": round(v_step), "achieved": round(g, 1),
+                             "frac": round(g / VALU_PEAK_G, 4),
                              "salu_insts_per_step": round(sq["salu_insts_per_iteration"]),
                              "salu_achieved": round(sq["salu_insts_per_iteration"] * K / main_res["elapsed"] / 1e9, 1)},
                      "source": "rocprofv3 SQ_INSTS_VALU / SQ_INSTS_SALU pass (profiles/pmc_latest.json)"}
@@ -439,10 +573,11 @@ def main():
                        "results": "bit-identical to the reference algorithm (oracle-checked at this size: "
                                   "tests/test_gpu_configs.py)" if args.accel != "bvh" else "exact closest hit",
                        "parallelism": f"samples sharded x{world}" + (" (gloo rehearsal)" if world > 1 and args.dist_backend == "gloo" else ""),
-                       "pipelines": main_res["pipes"],
+                       "pipelines": main_res["pipes"], "hw_queues": P.hw_queues(),
                        "segments": int(main_res["seg"]), "primary_segments_cached": int(main_res["seg_primary"]),
                        "segments_per_bounce_rank0": per_bounce,
                        "image_finite": main_res["img_ok"], "trace_faults": main_res["faults"]},
+            "full_run": full_rates(main_res, npix),
             "roofline": roof, "issue_roofline": issue, "cpu_baseline": cpu, "alt_mode": alt,
             "targets": targets or None,
         }

@@ -11,11 +11,11 @@
  *   pt_scene_add_mesh        <- Scene::processMesh                   Scene.cpp:264-291
  *   pt_scene_add_model       <- Model setup in Scene::Scene          Scene.cpp:32-42 (x11)
  *   pt_scene_build           <- Scene::addMeshesToGrid               Scene.cpp:318-396 (+ the per-mesh BLAS)
- *   pt_renderer_allocate_on_gpu <- Renderer::allocateOnGPU           Renderer.cpp:65-130, Renderer.h:371
+ *   pt_renderer_allocate_on_gpu <- Renderer::allocateOnGPU           Renderer.cpp:65-130, Renderer.h:49
  *   pt_renderer_clear_image  <- initImageKernel                      Renderer.cpp:557-565
- *   pt_renderer_render_loop  <- Renderer::renderLoop                 Renderer.cpp:567-648, Renderer.h:372
- *   pt_renderer_render_image <- Renderer::renderImage                Renderer.cpp:15-63, Renderer.h:373
- *   pt_renderer_free         <- Renderer::free                       Renderer.cpp:132-148, Renderer.h:374
+ *   pt_renderer_render_loop  <- Renderer::renderLoop                 Renderer.cpp:567-648, Renderer.h:50
+ *   pt_renderer_render_image <- Renderer::renderImage                Renderer.cpp:15-63, Renderer.h:51
+ *   pt_renderer_free         <- Renderer::free                       Renderer.cpp:132-148, Renderer.h:52
  *   pt_render                <- main()                               main.cpp:11-27
  *
  * Compile-time constants of Config.h (RESOLUTION_X/Y, ITER, GRID_X/Y/Z) and
@@ -35,9 +35,9 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 4
+#define PT_ABI_VERSION 5
 
-/* Primitive.h:213-222 Material::MaterialType */
+/* Primitive.h:70-79 Material::MaterialType */
 enum {
     PT_MAT_DIFFUSE = 0, PT_MAT_SPECULAR = 1, PT_MAT_REFLECTIVE = 2, PT_MAT_REFRACTIVE = 3,
     PT_MAT_EMISSIVE = 4, PT_MAT_COAT = 5, PT_MAT_METAL = 6
@@ -74,6 +74,11 @@ typedef struct pt_render_config {
 
 int pt_abi_version(void);
 const char *pt_last_error(void);
+/* GPU_MAX_HW_QUEUES as the library found it when it was loaded (*at_load = -1: unset)
+ * and whether the library then set it to 16 (*set_by_library = 1).  HIP reads the
+ * variable once, when its runtime starts: a process whose HIP runtime started before
+ * the library loaded runs with its own value (HIP's default is 4). */
+int pt_hw_queue_info(int *at_load, int *set_by_library);
 void pt_default_config(pt_render_config *cfg);
 
 /* ---- Scene ---- */

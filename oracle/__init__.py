@@ -33,7 +33,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libptoracle.so")
 
-# Primitive.h:213-222
+# Primitive.h:70-79
 MATERIALS = {
     "DIFFUSE": 0, "SPECULAR": 1, "REFLECTIVE": 2, "REFRACTIVE": 3,
     "EMISSIVE": 4, "COAT": 5, "METAL": 6,
@@ -247,7 +247,7 @@ def _geo_normal(p0, p1, p2):
 
 
 def _bbox_sequential(pos):
-    """BoundingBox() + update() over the vertices in order (Primitive.h:178-203):
+    """BoundingBox() + update() over the vertices in order (Primitive.h:35-60):
     min = min > v ? v : min starting at FLOAT_MAX (max symmetric at FLOAT_MIN).
     The survivor is the FIRST vertex holding the extreme value (keeps its sign
     of zero); NaN never replaces."""

@@ -30,7 +30,7 @@
 #include <omp.h>
 #endif
 
-/* Config.h:3-5 */
+/* Config.h:4-6 */
 #define OR_EPS 0.005f
 #define OR_FMAX 9999999.0f
 #define OR_FMIN -9999990.0f
@@ -38,7 +38,7 @@
 #define OR_TWO_PI 6.2831853071795864769252867665590057683943f
 #define OR_SQRT13 0.5773502691896257645091487805019574556476f
 
-/* Primitive.h:213-222 MaterialType */
+/* Primitive.h:70-79 MaterialType */
 enum { M_DIFFUSE = 0, M_SPECULAR, M_REFLECTIVE, M_REFRACTIVE, M_EMISSIVE, M_COAT, M_METAL };
 
 typedef struct { float x, y, z; } v3;

@@ -23,7 +23,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-__all__ = ["Scene", "Renderer", "RenderConfig", "PathTracerError", "build", "lib",
+__all__ = ["Scene", "Renderer", "RenderConfig", "PathTracerError", "build", "lib", "hw_queues",
            "MATERIALS", "ACCEL_GRID", "ACCEL_BVH", "ACCEL_GRID_FAST"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -35,7 +35,7 @@ ACCEL_GRID_FAST = 2
 # renderer.h: segments[] slots after the per-bounce counters, as segments_per_bounce indices
 _MAX_BOUNCE_COUNTERS = 64
 _DEFERRED_SLOT = 50 + _MAX_BOUNCE_COUNTERS - 1     # kDeferredRayCounter
-# Primitive.h:213-222
+# Primitive.h:70-79
 MATERIALS = {"DIFFUSE": 0, "SPECULAR": 1, "REFLECTIVE": 2, "REFRACTIVE": 3,
              "EMISSIVE": 4, "COAT": 5, "METAL": 6}
 
@@ -67,11 +67,13 @@ class _Cfg(ctypes.Structure):
 _P_F = ctypes.POINTER(ctypes.c_float)
 _P_I = ctypes.POINTER(ctypes.c_int)
 _lib = None
+_HIP_BEFORE_LOAD = None     # set when the library loads (torch's HIP runtime already up?)
 
 # (name, restype, argtypes) of every exported symbol of include/pathtracer_amd.h
 EXPORTS = [
     ("pt_abi_version", ctypes.c_int, []),
     ("pt_last_error", ctypes.c_char_p, []),
+    ("pt_hw_queue_info", ctypes.c_int, [_P_I, _P_I]),
     ("pt_default_config", None, [ctypes.POINTER(_Cfg)]),
     ("pt_scene_create", ctypes.c_void_p, []),
     ("pt_scene_destroy", None, [ctypes.c_void_p]),
@@ -117,6 +119,10 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(_LIB_PATH):
             raise PathTracerError(
                 f"{_LIB_PATH} not found: run `make -C pathtracerap_amd` (or __graft_entry__.build())")
+        global _HIP_BEFORE_LOAD
+        import sys
+        tc = sys.modules.get("torch.cuda")
+        _HIP_BEFORE_LOAD = bool(tc is not None and tc.is_initialized())
         L = ctypes.CDLL(_LIB_PATH)
         for name, res, args in EXPORTS:
             fn = getattr(L, name)
@@ -124,6 +130,20 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def hw_queues() -> dict:
+    """GPU_MAX_HW_QUEUES as the library found it at load (None: unset, then the
+    library set 16), and whether HIP had already started in this process when the
+    library loaded (then HIP runs with the value it read at its own start)."""
+    a, s = ctypes.c_int(), ctypes.c_int()
+    lib().pt_hw_queue_info(ctypes.byref(a), ctypes.byref(s))
+    libc = ctypes.CDLL(None)            # the C environment (os.environ is a snapshot taken at start-up)
+    libc.getenv.restype = ctypes.c_char_p
+    env = libc.getenv(b"GPU_MAX_HW_QUEUES")
+    env = env.decode() if env else None
+    return {"at_library_load": None if a.value < 0 else a.value, "set_by_library": bool(s.value),
+            "env_now": int(env) if env and env.isdigit() else None, "hip_started_before_load": _HIP_BEFORE_LOAD}
 
 
 def _err(rc, what):
@@ -282,7 +302,7 @@ def selftest_math(x, y) -> np.ndarray:
 
 
 class Renderer:
-    """Renderer (Renderer.h:368-377) on the gfx950 wavefront pipeline."""
+    """Renderer (Renderer.h:46-55) on the gfx950 wavefront pipeline."""
 
     def __init__(self, cfg: RenderConfig | None = None):
         self.cfg = cfg or RenderConfig()
@@ -395,3 +415,11 @@ def render(scene_config: str, cfg: RenderConfig | None = None, bmp_out: str | No
     (pt_default_config) overlaid with the scene file's RENDER block."""
     c = ctypes.byref(cfg.c()) if cfg is not None else None
     _err(lib().pt_render(os.fsencode(scene_config), c, os.fsencode(bmp_out) if bmp_out else None), "render")
+
+
+# Load the library when the package is imported: its load-time default
+# (GPU_MAX_HW_QUEUES=16, one hardware queue per pipeline stream) only takes
+# effect if it runs before the process starts HIP.  A missing library is not an
+# error here (build() may follow); every call into it raises.
+if os.path.exists(_LIB_PATH):
+    lib()

@@ -19,8 +19,18 @@ static thread_local std::string g_err;
 // the HIP runtime initialises: set it at load time unless the process already
 // chose a value.  (A process whose HIP runtime started before this library was
 // loaded keeps its own setting.)
+// What the process had chosen is recorded (pt_hw_queue_info), so a host can
+// report the queue count in effect or warn when it differs from the default.
+static int g_queues_at_load = -1;        // GPU_MAX_HW_QUEUES when the library loaded (-1: unset)
+static int g_queues_set_by_lib = 0;      // 1: the library set it (the process had not)
 __attribute__((constructor)) static void pt_default_hw_queues() {
-    setenv("GPU_MAX_HW_QUEUES", "16", /*overwrite=*/0);
+    const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+    if (e) {
+        g_queues_at_load = std::atoi(e);
+    } else {
+        setenv("GPU_MAX_HW_QUEUES", "16", /*overwrite=*/0);
+        g_queues_set_by_lib = 1;
+    }
 }
 
 static int set_err(const std::string& m) { g_err = m; return -1; }
@@ -28,6 +38,12 @@ static int set_err(const std::string& m) { g_err = m; return -1; }
 extern "C" {
 
 int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+int pt_hw_queue_info(int* at_load, int* set_by_library) {
+    if (at_load) *at_load = g_queues_at_load;
+    if (set_by_library) *set_by_library = g_queues_set_by_lib;
+    return 0;
+}
 const char* pt_last_error(void) { return g_err.c_str(); }
 
 void pt_default_config(pt_render_config* c) {

@@ -13,7 +13,7 @@
 
 namespace pt {
 
-// Config.h:3-5
+// Config.h:4-6
 constexpr float kEps = 0.005f;
 constexpr float kFMax = 9999999.0f;
 constexpr float kFMin = -9999990.0f;
@@ -21,7 +21,7 @@ constexpr float kFMin = -9999990.0f;
 constexpr float kTwoPi = 6.2831853071795864769252867665590057683943f;
 constexpr float kSqrtOneThird = 0.5773502691896257645091487805019574556476f;
 
-// Primitive.h:213-222 Material::MaterialType
+// Primitive.h:70-79 Material::MaterialType
 enum MaterialType : int {
     MAT_DIFFUSE = 0, MAT_SPECULAR = 1, MAT_REFLECTIVE = 2, MAT_REFRACTIVE = 3,
     MAT_EMISSIVE = 4, MAT_COAT = 5, MAT_METAL = 6

@@ -5,7 +5,7 @@
 
 namespace pt {
 
-// Primitive.h:252-257 SpatialAcceleration::EntityType
+// Primitive.h:109-114 SpatialAcceleration::EntityType
 enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2, ENTITY_SPHERE = 3 };
 
 // Acceleration structure used by the intersect stage.
@@ -23,7 +23,7 @@ enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2,
 //              ACCEL_GRID; needs the BVH.
 enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1, ACCEL_GRID_FAST = 2 };
 
-// One instance (Model, Primitive.h:237-244) flattened for the traces: 62
+// One instance (Model, Primitive.h:94-101) flattened for the traces: 62
 // dwords (the material, which only the shading pass reads, is ModelShade), so
 // k_trace_gf stages up to 12 of them in LDS at 16 resident waves per CU.
 struct ModelRec {
@@ -45,7 +45,7 @@ struct ModelRec {
 };
 static_assert(sizeof(ModelRec) == 62 * 4, "ModelRec layout");
 
-// The instance's material (Primitive.h:211-227), read by the shading pass.
+// The instance's material (Primitive.h:68-84), read by the shading pass.
 struct ModelShade {
     float color[3];       // Material::color
     int mat_type;         // Material::MaterialType

@@ -1,4 +1,4 @@
-// renderer.h -- MI355X wavefront renderer (Renderer.h:368-377 mirror).
+// renderer.h -- MI355X wavefront renderer (Renderer.h:46-55 mirror).
 //
 // allocateOnGPU / renderLoop / renderImage / free keep the reference's
 // entry points; underneath, each bounce is a persistent trace kernel

@@ -14,9 +14,9 @@
 
 namespace pt {
 
-struct Vertex { f3 position; f3 normal; };            // Primitive.h:166-171 (uv unused)
-struct Triangle { int vertex_indices[3]; };            // Primitive.h:173-176
-struct BoundingBox {                                   // Primitive.h:178-203
+struct Vertex { f3 position; f3 normal; };            // Primitive.h:23-28 (uv unused)
+struct Triangle { int vertex_indices[3]; };            // Primitive.h:30-33
+struct BoundingBox {                                   // Primitive.h:35-60
     f3 min = {kFMax, kFMax, kFMax};
     f3 max = {kFMin, kFMin, kFMin};
     void update(f3 v) {
@@ -28,18 +28,18 @@ struct BoundingBox {                                   // Primitive.h:178-203
         max.z = max.z < v.z ? v.z : max.z;
     }
 };
-struct IndexRange { int start_index = 0, end_index = 0; };    // Primitive.h:157-161
-struct Mesh { IndexRange vertex_indices, triangle_indices; BoundingBox bounding_box; };  // Primitive.h:229-234
-struct Material { int material_type = MAT_DIFFUSE; float color[3] = {1, 1, 1}; };       // Primitive.h:211-227
-struct Model {                                          // Primitive.h:237-244
+struct IndexRange { int start_index = 0, end_index = 0; };    // Primitive.h:14-18
+struct Mesh { IndexRange vertex_indices, triangle_indices; BoundingBox bounding_box; };  // Primitive.h:86-91
+struct Material { int material_type = MAT_DIFFUSE; float color[3] = {1, 1, 1}; };       // Primitive.h:68-84
+struct Model {                                          // Primitive.h:94-101
     int grid_index = -1;
     int mesh_index = 0;
     float model_to_world[16];                           // column-major glm::mat4
     float world_to_model[16];
     Material mat;
 };
-struct Voxel { IndexRange entity_index_range; int entity_type = ENTITY_TRIANGLE; };  // Primitive.h:266-270
-struct Grid {                                           // Primitive.h:272-282
+struct Voxel { IndexRange entity_index_range; int entity_type = ENTITY_TRIANGLE; };  // Primitive.h:123-127
+struct Grid {                                           // Primitive.h:129-139
     IndexRange voxelIndices;
     float voxel_width[3];
     int entity_type = ENTITY_MODEL;
@@ -73,7 +73,7 @@ public:
     // traverse it (grid_fast, bvh) when the scene was built grid-only.
     int ensureBvh();
 
-    // Scene.h:30-36
+    // Scene.h:26-32
     std::vector<Model> models;
     std::vector<Mesh> meshes;
     std::vector<Vertex> vertices;

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(pt_mod):
 
 def test_abi_version_and_defaults(pt_mod):
     L = pt_mod.lib()
-    assert L.pt_abi_version() == 4
+    assert L.pt_abi_version() == 5
     c = pt_mod._Cfg()
     L.pt_default_config(ctypes.byref(c))
     # Config.h / generateRaysKernel defaults
@@ -53,6 +53,21 @@ def test_library_load_sets_hw_queues_unless_chosen():
     env["GPU_MAX_HW_QUEUES"] = "4"
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
     assert out.strip() == "b'4'"
+
+
+def test_hw_queue_info_reports_the_setting_found_at_load():
+    """pt_hw_queue_info / hw_queues(): the value the process had chosen (or that
+    the library set 16); importing the package loads the library."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import pathtracerap_amd as P; print(P._lib is not None, "
+            "P.hw_queues())") % ROOT
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.startswith("True ") and "'at_library_load': None, 'set_by_library': True, 'env_now': 16" in out, out
+    env["GPU_MAX_HW_QUEUES"] = "4"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert "'at_library_load': 4, 'set_by_library': False, 'env_now': 4" in out, out
 
 
 def test_errors_are_reported_not_crashing(pt_mod):

@@ -88,3 +88,82 @@ def test_render_sharded_hip_two_ranks(gpu, pt_mod, oracle_mod, tmp_path):
     assert np.array_equal(single.view(np.uint32), want.view(np.uint32))
     assert np.abs(got).sum() > 0
     np.testing.assert_allclose(got, single, rtol=1e-6, atol=1e-6)
+
+
+README_WORKER = r"""
+import os, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+import torch
+import torch.distributed as dist
+import pathtracerap_amd as P
+from pathtracerap_amd.dist import render_sharded
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo")
+torch.cuda.set_device(0)
+s = P.Scene({scene!r})
+s.build()
+cfg = s.apply_settings(P.RenderConfig())
+cfg.width, cfg.height, cfg.pipelines = 2800, 2240, 2
+img = render_sharded(s, cfg, 2)                 # 1 + 1 iterations
+if rank == 0:
+    np.save({out!r}, img.cpu().numpy())
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def _run_ranks(script, n=2, timeout=300):
+    port = _free_port()
+    procs = []
+    for rank in range(n):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(n), LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=timeout)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+
+
+def test_configs3_readme_scene_sharded_two_ranks(gpu, pt_mod, oracle_mod, tmp_path):
+    """configs[3]'s workload: the README scene (Scene.cpp:3-224) at 2800x2240,
+    its samples sharded over ranks (here 2 iterations split 1 + 1 over two gloo
+    ranks sharing the GPU; RCCL over xGMI on the 8-GPU node) and the float3
+    accumulators sum-reduced: equals the oracle's 2-iteration render."""
+    from conftest import REF_SCENE
+    P, O = pt_mod, oracle_mod
+    out = str(tmp_path / "img.npy")
+    script = tmp_path / "worker_readme.py"
+    script.write_text(README_WORKER.format(root=ROOT, scene=REF_SCENE, out=out))
+    _run_ranks(script)
+    got = np.load(out).reshape(-1, 3)
+    s = P.Scene(REF_SCENE)
+    s.build()
+    cfg = s.apply_settings(P.RenderConfig())
+    cfg.width, cfg.height, cfg.iterations = 2800, 2240, 2
+    want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg, threads=16))
+    assert np.abs(got).sum() > 0
+    np.testing.assert_allclose(got, want, rtol=1e-6, atol=0)
+
+
+def test_bench_gpus_2_spawns_two_ranks(gpu):
+    """bench.py --gpus 2 without a launcher starts both ranks itself (here gloo,
+    two ranks on the one GPU) and reports the whole job: n_gpus == 2."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--steps", "2", "--warmup", "1", "--targets=", "--alt-accel=", "--no-cpu-baseline",
+                        "--no-full-runs", "--no-profile"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, p.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["trace_faults"] == 0
+    assert d["config"]["parallelism"].startswith("samples sharded x2")

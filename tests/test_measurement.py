@@ -93,3 +93,50 @@ def test_bench_workload_labels():
     assert b.workload_name(a).startswith("north_star target")
     a.ntri, a.bounces = 10_000_000, 16
     assert b.workload_name(a).startswith("configs[4]")
+
+
+def test_bench_full_rates():
+    """The full-spp render: spp iterations over all ranks in `seconds`."""
+    b = _bench()
+    res = {"full": {"spp": 256, "elapsed": 0.5, "seg": 1.0e9, "seg_primary": 2.5e8, "img_ok": True}}
+    f = b.full_rates(res, npix=1000)
+    assert f["spp"] == 256 and f["value"] == 2000.0 and f["traced_mrays_per_sec"] == 1500.0
+    assert f["samples_per_sec"] == 256 * 1000 / 0.5
+    assert b.full_rates({}, 1000) is None
+    assert b.SPP == {"configs1": 256, "target_1m": 1024, "configs2": 1024, "configs4": 4096}
+
+
+def test_bench_cpu_share_honours_the_pool_share(monkeypatch):
+    b = _bench()
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    n, why = b.host_cpu_share()
+    assert n == min(3, len(os.sched_getaffinity(0))) and "OMP_NUM_THREADS 3" in why
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    n, why = b.host_cpu_share()
+    assert n == len(os.sched_getaffinity(0)) or "cgroup" in why
+
+
+def _run_bench(args, env_extra, timeout=180):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_rejects_world_size_mismatch():
+    """Under a launcher the world size must equal --gpus (checked before any GPU call)."""
+    p = _run_bench(["--gpus", "3"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and "--gpus 3 but the launcher started 2" in p.stderr
+
+
+def test_bench_spawned_ranks_fail_together():
+    """--gpus 2 without a launcher starts two ranks itself; here (no GPU) both
+    fail, and the parent reports the failure with a non-zero exit instead of
+    hanging or printing a result line."""
+    p = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--steps", "1", "--warmup", "0", "--targets=",
+                    "--alt-accel=", "--no-cpu-baseline", "--no-full-runs", "--no-profile"], {})
+    assert p.returncode != 0
+    assert "exited with" in p.stderr
+    assert '"metric"' not in p.stdout

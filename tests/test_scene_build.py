@@ -139,3 +139,58 @@ def test_build_errors(pt_mod):
     s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
     with pytest.raises(pt_mod.PathTracerError, match="grid dimensions"):
         s.build(grid=(0, 25, 25))
+
+
+# --- addMeshesToGrid at the BASELINE.json sizes (Scene.cpp:293-396) -----------
+# The GPU-vs-oracle renders at 100k / 1M / 10M triangles feed the oracle the
+# product's exported scene, so the product's grid build must itself equal the
+# oracle's independent build_scene / ptor_build_grids at those sizes.
+
+def _synthetic_oracle_scene(oracle_mod, ntri, meshes=None):
+    """oracle.build_scene over synthetic.diffuse_scene's meshes and models
+    (BASE_MODEL_SCALE x1000 applied as the OBJ loader and addMesh do)."""
+    from pathtracerap_amd import synthetic as S
+    if meshes is None:
+        k = np.float32(1000)
+        meshes = [(p * k, n * k, t) for p, n, t in (S.room_mesh(), S.light_mesh(), S.torus_mesh(ntri))]
+    index = {"room": 0, "light": 1, "torus": 2}
+    models = [dict(mesh=index[m], scale=sc, rot=rot, translate=tr, material=mat[0], color=mat[1])
+              for m, tr, rot, sc, mat, _ in S._MODELS]
+    return oracle_mod.build_scene(meshes, models)
+
+
+@pytest.mark.parametrize("ntri", [100_000, 1_000_000, 10_000_000], ids=["configs1_100k", "target_1m", "configs4_10m"])
+def test_grid_build_bitexact_at_baseline_sizes(pt_mod, oracle_mod, ntri):
+    """In-memory build (Scene.addMesh / addModel: what bench.py's configs4 target
+    and the 10M parity tests use) vs the oracle's build, every exported vector."""
+    from pathtracerap_amd import synthetic as S
+    s = S.build_scene(pt_mod, ntri, bvh=False)
+    a = s.export()
+    del s
+    o = _synthetic_oracle_scene(oracle_mod, ntri)
+    assert a["tris"].shape[0] >= 0.99 * ntri
+    _compare(a, o)
+
+
+@pytest.mark.parametrize("ntri", [100_000, 1_000_000], ids=["configs1_100k", "target_1m"])
+def test_grid_build_bitexact_obj_route(tmp_path, pt_mod, oracle_mod, ntri):
+    """The OBJ route the bench's configs[1] and 1M-target scenes take
+    (synthetic.diffuse_scene -> Config.txt grammar -> OBJ loader): the grid the
+    product builds over the loaded meshes equals the oracle's build over the
+    same vertex arrays; at 100k the loader itself is checked against
+    oracle.load_obj too."""
+    from pathtracerap_amd import synthetic as S
+    path = S.diffuse_scene(str(tmp_path), ntri=ntri)
+    s = pt_mod.Scene(path)
+    s.build(bvh=False)
+    a = s.export()
+    r = a["mesh_ranges"]
+    # the scene file's OBJ blocks: room, light, torus (mesh order)
+    meshes = [(a["vpos"][v0:v1], a["vnrm"][v0:v1], a["tris"][t0:t1] - v0) for v0, v1, t0, t1 in r]
+    if ntri <= 100_000:
+        for (p, n, t), name in zip(meshes, ["room.obj", "light.obj", f"torus_{ntri}_0.obj"]):
+            op, on, ot = oracle_mod.load_obj(os.path.join(str(tmp_path), name))
+            assert_bitexact(p, op, name + " positions")
+            assert_bitexact(n, on, name + " normals")
+            assert_bitexact(t, ot, name + " triangles")
+    _compare(a, _synthetic_oracle_scene(oracle_mod, ntri, meshes))
