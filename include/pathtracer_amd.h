@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5
+#define PT_ABI_VERSION 6
 
 /* Primitive.h:70-79 Material::MaterialType */
 enum {
@@ -109,11 +109,6 @@ int pt_scene_export(const pt_scene *s, float *vpos, float *vnrm, int *tris, int 
 /* BVH export (ACCEL_BVH builds): nodes nbvh_nodes*16 (the 64-byte BvhNode as
  * 16 floats; int fields bit-cast), refs nbvh_refs, roots nmesh. */
 int pt_scene_export_bvh(const pt_scene *s, float *nodes, int *refs, int *roots);
-/* 4-wide BLAS (the binary one collapsed; used by the persistent trace kernels):
- * *n_nodes = node count; nodes n_nodes*32 (the 128-byte Bvh4Node as 32 floats:
- * lox[4] hix[4] loy[4] hiy[4] loz[4] hiz[4], then link[4] cnt[4] bit-cast), roots nmesh.
- * Either array may be NULL. */
-int pt_scene_export_bvh4(const pt_scene *s, int *n_nodes, float *nodes, int *roots);
 
 /* ---- Renderer ---- */
 pt_renderer *pt_renderer_create(const pt_render_config *cfg);

@@ -87,7 +87,6 @@ EXPORTS = [
     ("pt_scene_export", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_F, _P_I, _P_I, _P_F, _P_I, _P_F, _P_F,
                                        _P_F, _P_I, _P_F, _P_I, _P_I]),
     ("pt_scene_export_bvh", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_I, _P_I]),
-    ("pt_scene_export_bvh4", ctypes.c_int, [ctypes.c_void_p, _P_I, _P_F, _P_I]),
     ("pt_renderer_create", ctypes.c_void_p, [ctypes.POINTER(_Cfg)]),
     ("pt_renderer_set_stream", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("pt_renderer_bind_image", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -280,17 +279,6 @@ def _scene_export_bvh(self) -> dict:
 Scene.export_bvh = _scene_export_bvh
 
 
-def _scene_export_bvh4(self) -> dict:
-    n = self.counts()
-    cnt = np.zeros(1, np.int32)
-    _err(lib().pt_scene_export_bvh4(self._h, _ip(cnt), None, None), "export_bvh4")
-    nodes = np.zeros((max(int(cnt[0]), 1), 32), np.float32)
-    roots = np.zeros(max(n["nmesh"], 1), np.int32)
-    _err(lib().pt_scene_export_bvh4(self._h, _ip(cnt), _fp(nodes), _ip(roots)), "export_bvh4")
-    return dict(nodes=nodes[:int(cnt[0])], roots=roots[:n["nmesh"]])
-
-
-Scene.export_bvh4 = _scene_export_bvh4
 
 
 def selftest_math(x, y) -> np.ndarray:

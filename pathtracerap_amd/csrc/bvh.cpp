@@ -274,170 +274,4 @@ int Scene::relayoutPairs(int n0, int root) {
     return nid[root - n0];
 }
 
-namespace {
-
-struct Slot {            // one child of the binary BLAS, as stored in its parent
-    float lo[3], hi[3];
-    int link, count;     // count: -1 empty, 0 inner (link = BvhNode), > 0 leaf
-};
-
-double slot_area(const Slot& c) {
-    const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
-    return 2.0 * (dx * dy + dy * dz + dz * dx);
-}
-
-Slot child_of(const BvhNode& n, int c) {
-    Slot s;
-    for (int k = 0; k < 3; k++) {
-        s.lo[k] = c == 0 ? n.lo0[k] : n.lo1[k];
-        s.hi[k] = c == 0 ? n.hi0[k] : n.hi1[k];
-    }
-    s.link = c == 0 ? n.link0 : n.link1;
-    s.count = c == 0 ? n.count0 : n.count1;
-    return s;
-}
-
-struct Collapser {
-    Scene& s;
-    explicit Collapser(Scene& sc) : s(sc) {}
-
-    // Builds the BVH4 node for a set of up to 4 slots; returns its index.
-    int emit(std::vector<Slot> kids, int depth) {
-        const int idx = (int)s.bvh4_nodes.size();
-        s.bvh4_nodes.push_back(Bvh4Node());
-        s.bvh4_max_depth = std::max(s.bvh4_max_depth, depth);
-        Bvh4Node nd;
-        for (int c = 0; c < 4; c++) {
-            nd.lox[c] = nd.loy[c] = nd.loz[c] = 1.0f;
-            nd.hix[c] = nd.hiy[c] = nd.hiz[c] = -1.0f;
-            nd.link[c] = -1;
-            nd.cnt[c] = -1;
-        }
-        for (size_t c = 0; c < kids.size(); c++) {
-            const Slot& k = kids[c];
-            nd.lox[c] = k.lo[0]; nd.loy[c] = k.lo[1]; nd.loz[c] = k.lo[2];
-            nd.hix[c] = k.hi[0]; nd.hiy[c] = k.hi[1]; nd.hiz[c] = k.hi[2];
-            if (k.count > kBvh4LeafMax) {
-                // oversized leaf (binary BLAS depth cap): chunks of <= kBvh4LeafMax under one node
-                std::vector<Slot> chunks;
-                for (int st = 0; st < k.count; st += kBvh4LeafMax) {
-                    Slot ch = k;
-                    ch.link = k.link + st;
-                    ch.count = std::min(kBvh4LeafMax, k.count - st);
-                    chunks.push_back(ch);
-                }
-                nd.link[c] = build_from(chunks, depth + 1);
-                nd.cnt[c] = 0;
-            } else if (k.count == 0) {
-                nd.link[c] = collapse(s.bvh_nodes[k.link], depth + 1);
-                nd.cnt[c] = 0;
-            } else {
-                nd.link[c] = k.link;
-                nd.cnt[c] = k.count;
-            }
-        }
-        s.bvh4_nodes[idx] = nd;
-        return idx;
-    }
-
-    // Up to 4 slots per node; more (leaf chunks) are grouped recursively.
-    int build_from(std::vector<Slot> kids, int depth) {
-        if (kids.size() <= 4) return emit(kids, depth);
-        std::vector<Slot> groups;
-        for (size_t g = 0; g < kids.size(); g += 4) {
-            std::vector<Slot> part(kids.begin() + g, kids.begin() + std::min(kids.size(), g + 4));
-            Slot grp = part[0];
-            for (const Slot& q : part)
-                for (int k = 0; k < 3; k++) { grp.lo[k] = std::min(grp.lo[k], q.lo[k]); grp.hi[k] = std::max(grp.hi[k], q.hi[k]); }
-            grp.count = -2;                       // placeholder: filled below
-            groups.push_back(grp);
-            (void)part;
-        }
-        // emit the groups as child nodes
-        std::vector<Slot> top;
-        for (size_t g = 0, gi = 0; g < kids.size(); g += 4, gi++) {
-            std::vector<Slot> part(kids.begin() + g, kids.begin() + std::min(kids.size(), g + 4));
-            Slot t = groups[gi];
-            t.count = 0;
-            t.link = -1;
-            top.push_back(t);
-            top.back().link = emit(part, depth + 1);
-        }
-        return emit_inner(top, depth);
-    }
-
-    // Node whose children are already-emitted BVH4 nodes.
-    int emit_inner(const std::vector<Slot>& kids, int depth) {
-        if (kids.size() > 4) return build_from_inner(kids, depth);
-        const int idx = (int)s.bvh4_nodes.size();
-        s.bvh4_nodes.push_back(Bvh4Node());
-        s.bvh4_max_depth = std::max(s.bvh4_max_depth, depth);
-        Bvh4Node nd;
-        for (int c = 0; c < 4; c++) {
-            nd.lox[c] = nd.loy[c] = nd.loz[c] = 1.0f;
-            nd.hix[c] = nd.hiy[c] = nd.hiz[c] = -1.0f;
-            nd.link[c] = -1;
-            nd.cnt[c] = -1;
-        }
-        for (size_t c = 0; c < kids.size(); c++) {
-            nd.lox[c] = kids[c].lo[0]; nd.loy[c] = kids[c].lo[1]; nd.loz[c] = kids[c].lo[2];
-            nd.hix[c] = kids[c].hi[0]; nd.hiy[c] = kids[c].hi[1]; nd.hiz[c] = kids[c].hi[2];
-            nd.link[c] = kids[c].link;
-            nd.cnt[c] = 0;
-        }
-        s.bvh4_nodes[idx] = nd;
-        return idx;
-    }
-
-    int build_from_inner(const std::vector<Slot>& kids, int depth) {
-        std::vector<Slot> top;
-        for (size_t g = 0; g < kids.size(); g += 4) {
-            std::vector<Slot> part(kids.begin() + g, kids.begin() + std::min(kids.size(), g + 4));
-            Slot t = part[0];
-            for (const Slot& q : part)
-                for (int k = 0; k < 3; k++) { t.lo[k] = std::min(t.lo[k], q.lo[k]); t.hi[k] = std::max(t.hi[k], q.hi[k]); }
-            t.count = 0;
-            t.link = emit_inner(part, depth + 1);
-            top.push_back(t);
-        }
-        return emit_inner(top, depth);
-    }
-
-    // Children of binary node n, expanded (largest-area inner child first) until 4.
-    int collapse(const BvhNode& n, int depth) {
-        std::vector<Slot> kids;
-        for (int c = 0; c < 2; c++) {
-            const Slot k = child_of(n, c);
-            if (k.count >= 0) kids.push_back(k);
-        }
-        for (;;) {
-            if (kids.size() >= 4) break;
-            int pick = -1;
-            double best = -1.0;
-            for (size_t i = 0; i < kids.size(); i++)
-                if (kids[i].count == 0 && slot_area(kids[i]) > best) { best = slot_area(kids[i]); pick = (int)i; }
-            if (pick < 0) break;
-            const BvhNode& inner = s.bvh_nodes[kids[pick].link];
-            kids.erase(kids.begin() + pick);
-            for (int c = 0; c < 2; c++) {
-                const Slot k = child_of(inner, c);
-                if (k.count >= 0) kids.push_back(k);
-            }
-        }
-        return emit(kids, depth);
-    }
-};
-
-}  // namespace
-
-// The mesh's binary BLAS collapsed into 4-wide nodes.  Child boxes are the
-// binary nodes' (already tolerance-grown, rounded-outward) boxes, so the 4-wide
-// traversal prunes exactly as conservatively as the binary one.
-void Scene::buildBvh4(int mesh) {
-    const int root2 = mesh_bvh_root[mesh];
-    if (root2 < 0) return;
-    Collapser C(*this);
-    mesh_bvh4_root[mesh] = C.collapse(bvh_nodes[root2], 1);
-}
-
 }  // namespace pt

@@ -38,7 +38,7 @@ struct ModelRec {
     int bvh_root;         // index of the mesh's BLAS root node
     float wbox[6];        // conservative world-space AABB of everything the instance can hit
     float reach;          // R: max over triangles of the (tolerance-grown) voxel-box diameter, model units
-    int bvh4_root;        // index of the mesh's 4-wide BLAS root node
+    int pad0;             // (was the 4-wide BLAS root; keeps the 62-dword record)
     float wdelta;         // tier-1 window: the walk is exact up to t_min + wdelta
     float ivw[3];         // 1 / vw (rounded; walk certificate only, used with margins)
     float cslack[3];      // walk certificate: position slack per axis (DDA +EPSILON shift + rounding)
@@ -62,16 +62,5 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
 
-// 4-wide BVH node (the binary BLAS collapsed two levels at a time): child
-// boxes as SoA rows so the four slab tests vectorise, 128 bytes.
-// cnt[c] == -1 empty slot, 0 -> link[c] is a Bvh4Node index, > 0 -> link[c]
-// is the first bvh_tri_geom record of a leaf of cnt[c] (<= kBvh4LeafMax) triangles.
-constexpr int kBvh4LeafMax = 7;
-struct Bvh4Node {
-    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
-    int link[4];
-    int cnt[4];
-};
-static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 
 }  // namespace pt

@@ -47,7 +47,6 @@ struct KParams {
     const BvhNode* bvh;
     const int* bvh_tri;
     const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
-    const Bvh4Node* bvh4;       // 4-wide BLAS (persistent traces)
     int* spill;                 // traversal-stack spill beyond the LDS entries, lane-minor
     int spill_stride;           // lanes in the spill layout
     // frame
@@ -71,7 +70,7 @@ struct KParams {
     int* hitm;                          // per-slot model
     int* trace_next;                    // persistent trace: next unclaimed source block, reset by k_scan
     int trace_refill;                   // refill a wave's idle lanes once this many are idle
-    int trace_flags;                    // k_trace_bvh variant: 1 LDS model records, 2 leaf steps, 4 block claims
+    int trace_flags;                    // k_trace_bvh variant: 11 LDS model records, 10 global
     int* defer_slots;                   // k_trace_gf: slots whose hit set overflowed LDS (k_trace_deferred)
     int* defer_count;                   // reset by k_scan
     float* contrib;                     // pipelines > 1: this pipeline's per-iteration contributions (k_merge)
@@ -79,14 +78,7 @@ struct KParams {
     int* sort_bins;                     // [kSortBins] rays per key, [kSortBins] scatter cursors; zeroed by k_scan
     unsigned short* sort_key;           // per source index of the previous bounce's pool
     int sort_mode;                      // key layout (k_sort_hist); 0 = no sort
-    int hit_order;                      // 1: hit records at claim positions, slot_pos[j] = j's position (PT_HIT_ORDER)
-    int* slot_pos;
-    float4* sray;                       // PT_SORT_COPY: rays in claim order, 2 float4 per position:
-                                        // (o.xyz, dense slot as int bits), (d.xyz, bounces); null: gather via order
-    int sort_copy;                      // 1: k_sort_scatter writes sray (PT_SORT_COPY)
     float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
-    int* slot_src;                      // dense slot -> source index in the previous bounce's pool (k_slotmap)
-    int use_slotmap;                    // 1: slot_source reads slot_src (PT_SLOTMAP, default on)
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
     int* cont;                          // drain continuations: rays a persistent trace handed on (SoA, stride cont_cap)
     int cont_cap;
@@ -98,11 +90,6 @@ struct KParams {
                                         // hands nothing on.  Record buffers alternate between levels
     int drain_dump;                     // hand a wave's rays on once the pool is exhausted and <= this many
                                         // lanes still trace (0: off; PT_DRAIN_DUMP overrides)
-    const int4* qnodes;                 // k_trace_gf (PT_GF_QNODES): the binary BLAS with 16-bit child planes, 32 B
-                                        // per node, same indices (2 x int4: 12 planes, link|count words)
-    const float4* qframe;               // per mesh: (lo.xyz, -), (scale.xyz, -): plane = lo + q * scale
-    const float4* top_nodes;            // k_trace_gf (PT_GF_TOP > 0): the top BLAS levels of mesh top_mesh, BFS
-    int top_mesh;                       // order, staged in LDS (inner links into the table carry kTopFlag)
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,
                                         // counted in segments[kTraceFaultCounter]); PT_TRACE_ITER_CAP overrides
 };

@@ -40,48 +40,15 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP
 #define PT_HITCAP 6
 #endif
-#ifndef PT_WALK_CERT
-#define PT_WALK_CERT 1        // decide the common grid_fast walk from the ray's geometry (walk_certify)
-#endif
-#ifndef PT_CERT_FILTER
-#define PT_CERT_FILTER 1      // walk certificate: U over the members not provably entered after B* (walk_certify)
-#endif
-#ifndef PT_CERT_INSIDE
-#define PT_CERT_INSIDE 0      // walk certificate: U = B* without the filter when every member's box lies in B*
-#endif
-#ifndef PT_WALK_SKIP
-#define PT_WALK_SKIP 1        // fast-forward the grid_fast walk to the members' union box (walk_skip)
-#endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
 #endif
 #ifndef PT_MINWAVES
 #define PT_MINWAVES 5
 #endif
-#ifndef PT_XCD_MAP
-#define PT_XCD_MAP 0      // 1: XCD-contiguous chunk mapping (measured 20% slower: off)
-#endif
-#ifndef PT_FMA_NODES
-#define PT_FMA_NODES 1    // node slab tests as fma(lo, inv, -o*inv): +1-2 % in the persistent traces (0: sub + mul)
-#endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
-#ifndef PT_SORT_BITS
-#define PT_SORT_BITS 12       // ray sort key bits (14: key 9, 15: key 10 -- finer cells, bigger LDS histograms)
-#endif
-constexpr int kSortBits = PT_SORT_BITS, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
-#ifndef PT_SORT_COPY
-#define PT_SORT_COPY 0        // default of the PT_SORT_COPY env switch (rays copied to their claim positions)
-#endif
-constexpr bool kSortCopyDefault = PT_SORT_COPY != 0;
-// PT_LATE_RAY: k_trace_gf's refill claims and reads the claim-order entry as before, but
-// the ray gather of the refilled lanes (state 8) is issued inside the next node step,
-// right after that step's node loads: vmcnt retires in issue order, so the node step
-// waits only for its own loads and the gather overlaps its arithmetic.  Any other
-// phase gathers at once, as without the option.
-#ifndef PT_LATE_RAY
-#define PT_LATE_RAY 0
-#endif
+constexpr int kSortBits = 12, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
 #ifndef PT_SORT_WG
 #define PT_SORT_WG 512
 #endif
@@ -101,50 +68,6 @@ constexpr int kScanWG = PT_SCAN_WG, kScanPer = 8;                   // k_scan: o
 // Device helpers
 // ---------------------------------------------------------------------------
 struct Hit { float dist; f3 n; int model; };
-
-// Streaming (non-temporal) access to the ray pools (PT_RAY_NT bits): 1 the
-// persistent traces' refill gathers (ray + claim-order entry), 2 the shading
-// pass's ray / hit reads and ray writes, 4 the sort's ray reads.  Ray data is
-// touched once per pass; marked non-temporal it need not displace the BLAS
-// lines the traces re-read from L2.
-#ifndef PT_RAY_NT
-#define PT_RAY_NT 0
-#endif
-// Ray pool layout (PT_RAY_AOS): 0 = planes (o, pixel) and (d, bounces) apart (two
-// L2 lines per ray gathered by a trace refill); 1 = the two interleaved per ray, 32
-// contiguous bytes (one line).  Plane q of ray i is p.ray[buf][q][kRS * i].
-#ifndef PT_RAY_AOS
-#define PT_RAY_AOS 0
-#endif
-constexpr int kRS = PT_RAY_AOS ? 2 : 1;
-typedef float v4f_t __attribute__((ext_vector_type(4)));
-typedef int v2i_t __attribute__((ext_vector_type(2)));
-template <int BIT>
-__device__ __forceinline__ float4 ld_ray(const float4* q) {
-    if (PT_RAY_NT & BIT) {
-        const v4f_t v = __builtin_nontemporal_load(reinterpret_cast<const v4f_t*>(q));
-        return make_float4(v.x, v.y, v.z, v.w);
-    }
-    return *q;
-}
-template <int BIT>
-__device__ __forceinline__ int2 ld_ord(const int2* q) {
-    if (PT_RAY_NT & BIT) {
-        const v2i_t v = __builtin_nontemporal_load(reinterpret_cast<const v2i_t*>(q));
-        return make_int2(v.x, v.y);
-    }
-    return *q;
-}
-template <int BIT>
-__device__ __forceinline__ void st_ray(float4* q, float4 v) {
-    if (PT_RAY_NT & BIT) {
-        v4f_t w;
-        w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
-        __builtin_nontemporal_store(w, reinterpret_cast<v4f_t*>(q));
-    } else {
-        *q = v;
-    }
-}
 
 // computeRayBoundingBoxIntersection (Renderer.cpp:150-170)
 __device__ __forceinline__ bool slab_ref(const float* bb, f3 o, f3 d, f3 inv, float& t) {
@@ -263,16 +186,9 @@ __device__ bool grid_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3
 
 // Inverse direction for node tests: clamped to +-1e30 so the FMA form never
 // meets inf * 0 or inf - inf (a zero direction component stays a huge slope).
-// Slopes for the instance culling (model_culled): hardware reciprocals (v_rcp_f32,
-// 1 ulp) instead of correctly rounded divisions (about 10 instructions each).
-// The culling test only has to be conservative, and the world boxes it tests
-// are padded by 1e-4 of their diagonal + 0.01 (plus 1e-3 of the mesh diagonal
-// + 1 before the transform), far beyond a few ulps of the slab parameters.
-#ifndef PT_CULL_RCP
-#define PT_CULL_RCP 0       // measured neutral (README scene -0.5 % / +0.5 %): exact divisions stay
-#endif
+// Slopes for the instance culling are correctly rounded divisions (hardware
+// reciprocals measured neutral in round 3; DESIGN.md "Pruned variants").
 __device__ __forceinline__ f3 cull_inv(f3 d) {
-    if (PT_CULL_RCP) return mk3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     return mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 }
 __device__ __forceinline__ f3 node_inv(f3 inv) {
@@ -283,16 +199,10 @@ __device__ __forceinline__ f3 node_inv(f3 inv) {
 // so the test need not follow the reference's rounding: the FMA form
 // lo * inv - o * inv is used, with o * inv hoisted per traversal).
 __device__ __forceinline__ void node_slab(const float* lo, const float* hi, f3 o, f3 inv, float& tn, float& tf) {
-#if PT_FMA_NODES
     const f3 oi = o * inv;   // recomputed per call; the compiler hoists it out of the traversal loop
     float a0 = __builtin_fmaf(lo[0], inv.x, -oi.x), b0 = __builtin_fmaf(hi[0], inv.x, -oi.x);
     float a1 = __builtin_fmaf(lo[1], inv.y, -oi.y), b1 = __builtin_fmaf(hi[1], inv.y, -oi.y);
     float a2 = __builtin_fmaf(lo[2], inv.z, -oi.z), b2 = __builtin_fmaf(hi[2], inv.z, -oi.z);
-#else
-    float a0 = (lo[0] - o.x) * inv.x, b0 = (hi[0] - o.x) * inv.x;
-    float a1 = (lo[1] - o.y) * inv.y, b1 = (hi[1] - o.y) * inv.y;
-    float a2 = (lo[2] - o.z) * inv.z, b2 = (hi[2] - o.z) * inv.z;
-#endif
     tn = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fminf(a2, b2));
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
 }
@@ -714,7 +624,6 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
     // harmless, and one exit saves the scalar exec-mask work of eight divergent returns.
     bool ok = true;
 #define PT_CERT_FAIL(r) { if (PT_TRACE_STATS && (p.debug & 4) && ok) atomicAdd(p.segments + 32 + (r) + kMaxBounceCounters, 1ull); ok = false; }
-#if PT_CERT_FILTER
     // U is the union over the members the walk might enter no later than B*
     // (the minimum-t members' union box); members whose box it provably enters
     // only after B* cannot make a voxel before B*'s first one a hit voxel, so
@@ -731,26 +640,6 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
     }
     if (cnt == 0) PT_CERT_FAIL(0)
     if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) PT_CERT_FAIL(1)
-#if PT_CERT_INSIDE
-    // A member whose voxel box lies inside B* adds nothing to U (B* is part of U),
-    // so it needs no entry test.  When every member is such (one member; or the
-    // common pair of a slab's faces in the same voxels), U = B* and the filter below
-    // -- a grown-box entry per member -- is skipped.
-    auto inside_b = [&](const int4 e) {
-        return (e.z & 1023) >= blx && ((e.z >> 10) & 1023) >= bly && ((e.z >> 20) & 1023) >= blz &&
-               (e.w & 1023) <= bhx && ((e.w >> 10) & 1023) <= bhy && ((e.w >> 20) & 1023) <= bhz;
-    };
-    bool need = false;
-#pragma unroll
-    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
-        if (CAP > 0 && h >= nh) break;
-        const int4 e = get(h);
-        need = need | (!(__int_as_float(e.x) == tmin) & !inside_b(e));
-    }
-    if (!need) {
-        ulx = blx; uly = bly; ulz = blz; uhx = bhx; uhy = bhy; uhz = bhz;
-    } else
-#endif
     {
         // sB: exact-ray entry parameter (from pt) of B*.  The walk enters its first
         // voxel of B* at a computed parameter <= sB + errm (errm: the largest
@@ -785,11 +674,7 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
             if (CAP > 0 && h >= nh) break;
             const int4 e = get(h);
             bool in = true;
-#if PT_CERT_INSIDE
-            if (use && __int_as_float(e.x) != tmin && !inside_b(e)) {
-#else
             if (use && __int_as_float(e.x) != tmin) {
-#endif
                 float g = -3.0e38f, go = 3.0e38f;
 #pragma unroll
                 for (int a = 0; a < 3; a++) {
@@ -809,18 +694,6 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
             uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
         }
     }
-#else
-#pragma unroll
-    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
-        if (CAP > 0 && h >= nh) break;
-        const int4 e = get(h);
-        if (__int_as_float(e.x) == tmin) cnt++;
-        ulx = min(ulx, e.z & 1023); uly = min(uly, (e.z >> 10) & 1023); ulz = min(ulz, (e.z >> 20) & 1023);
-        uhx = max(uhx, e.w & 1023); uhy = max(uhy, (e.w >> 10) & 1023); uhz = max(uhz, (e.w >> 20) & 1023);
-    }
-    if (cnt == 0) PT_CERT_FAIL(0)
-    if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f) PT_CERT_FAIL(1)
-#endif
     const float dd[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z}, pp[3] = {pt.x, pt.y, pt.z};
     const int ul[3] = {ulx, uly, ulz}, uh[3] = {uhx, uhy, uhz};
     float sin = -3.0e38f, sout = 3.0e38f;
@@ -886,7 +759,6 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
 template <int CAP, class GetM, bool CERT = true, bool STRICT = false>
 __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                                     GetM get, int nh, float tmin, float win) {
-#if PT_WALK_CERT
     if (CERT) {
         int tri;
         if (walk_certify<CAP>(p, M, d, inv, pt, t_box, get, nh, tmin, win, tri)) {
@@ -896,16 +768,13 @@ __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const Mode
             return r;
         }
     }
-#endif
     const bool stamps = PT_TRACE_STATS && (p.debug & 64);     // wave cycles: init+union, skip, steps
     unsigned long long c0 = stamps ? clock64() : 0;
     Walk w;
     walk_init(p, M, d, inv, pt, w);
     walk_union_g<CAP>(get, nh, w);
     unsigned long long c1 = stamps ? clock64() : 0;
-#if PT_WALK_SKIP
     walk_skip(d, w);
-#endif
     unsigned long long c2 = stamps ? clock64() : 0;
     unsigned steps = 1;
     while (!walk_step_g<CAP, GetM, STRICT>(p, d, get, nh, tmin, w)) steps++;
@@ -1077,47 +946,25 @@ __device__ __forceinline__ Hit make_hit(const KParams& p, float gdist, int gmode
     return h;
 }
 
-// Hit record of the split trace -> shade path (p.hit4 / p.hitm, slot j).
-// PT_HIT_TRI = 0: (dist, world normal) + model, the normal computed by the trace.
-// PT_HIT_TRI = 1: (dist, triangle) + model; the shading pass fetches the triangle
-// normal and transforms it (make_hit's float operations, so the same values):
-// the latency-bound trace loses a dependent gather and the transform.
-#ifndef PT_HIT_TRI
-#define PT_HIT_TRI 1
-#endif
-__device__ __forceinline__ void put_hit(const KParams& p, int j, float gdist, int gmodel, int gtri,
-                                        const ModelRec* models) {
-    if (PT_HIT_TRI) {
-        const bool any = gdist < kFMax;
-        p.hit4[j] = make_float4(any ? gdist : kFMax, __int_as_float(gtri), 0.0f, 0.0f);
-        p.hitm[j] = any ? gmodel : -1;
-        return;
-    }
-    Hit h;
-    h.dist = kFMax; h.n = mk3(0, 0, 0); h.model = -1;
-    if (gdist < kFMax) {
-        const float4 tn = gtri >= 0 ? p.tri_normal[gtri] : make_float4(0, 0, 0, 0);
-        h.dist = gdist;
-        h.model = gmodel;
-        h.n = normalize(xform_normal9(models[gmodel].nm, mk3(tn.x, tn.y, tn.z)));
-    }
-    p.hit4[j] = make_float4(h.dist, h.n.x, h.n.y, h.n.z);
-    p.hitm[j] = h.model;
+// Hit record of the split trace -> shade path (p.hit4 / p.hitm, slot j):
+// (dist, triangle) + model.  The shading pass fetches the triangle normal and
+// transforms it with make_hit's float operations (the same values): the
+// latency-bound trace does no dependent normal gather (round 3, +1-2 %).
+__device__ __forceinline__ void put_hit(const KParams& p, int j, float gdist, int gmodel, int gtri) {
+    const bool any = gdist < kFMax;
+    p.hit4[j] = make_float4(any ? gdist : kFMax, __int_as_float(gtri), 0.0f, 0.0f);
+    p.hitm[j] = any ? gmodel : -1;
 }
 __device__ __forceinline__ Hit get_hit(const KParams& p, int hj) {
-    const float4 hh = ld_ray<2>(p.hit4 + hj);
+    const float4 hh = p.hit4[hj];
     Hit h;
     h.dist = hh.x;
     h.model = p.hitm[hj];
-    if (PT_HIT_TRI) {
-        h.n = mk3(0, 0, 0);
-        if (h.model >= 0) {
-            const int tri = __float_as_int(hh.y);
-            const float4 tn = tri >= 0 ? p.tri_normal[tri] : make_float4(0, 0, 0, 0);
-            h.n = normalize(xform_normal9(p.models[h.model].nm, mk3(tn.x, tn.y, tn.z)));
-        }
-    } else {
-        h.n = mk3(hh.y, hh.z, hh.w);
+    h.n = mk3(0, 0, 0);
+    if (h.model >= 0) {
+        const int tri = __float_as_int(hh.y);
+        const float4 tn = tri >= 0 ? p.tri_normal[tri] : make_float4(0, 0, 0, 0);
+        h.n = normalize(xform_normal9(p.models[h.model].nm, mk3(tn.x, tn.y, tn.z)));
     }
     return h;
 }
@@ -1240,7 +1087,6 @@ __global__ __launch_bounds__(kBlock) void k_intersect_rays(KParams p, int n, con
 // Dense slot j of bounce `bounce` -> its index in the ray pool written by the
 // previous bounce (block-local compaction + k_scan offsets).
 __device__ __forceinline__ int slot_source(const KParams& p, int j) {
-    if (p.use_slotmap) return p.slot_src[j];        // one load instead of the search below
     const int chunk = j / p.chunk;
     int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
     while (lo < hi) {
@@ -1268,18 +1114,6 @@ __device__ __forceinline__ void spush_t(int* stack, int* spill, int stride, int 
     if (sp < SCAP) stack[sp * BS] = e;
     else spill[(size_t)(sp - SCAP) * stride] = e;
 }
-template <int BS, int SCAP = kStack>
-__device__ __forceinline__ int spop_t(const int* stack, const int* spill, int stride, int sp) {
-    // Written as a select of the two addresses, the compiler merged the loads
-    // into one flat load (which waits on both the LDS and the vector memory
-    // counters) on every pop.  Typed LDS / global pointers keep them apart: the
-    // LDS read is unconditional (clamped index), the spill read has its own branch.
-    typedef __attribute__((address_space(3))) const int lds_int;
-    typedef __attribute__((address_space(1))) const int glb_int;
-    int v = ((lds_int*)stack)[min(sp, SCAP - 1) * BS];
-    if (sp >= SCAP) v = ((glb_int*)spill)[(size_t)(sp - SCAP) * stride];
-    return v;
-}
 // Pop for the lanes with `take`, without a branch around the LDS read: every lane
 // reads its (clamped) LDS entry; only a spilled entry is read under a branch.
 template <int BS, int SCAP = kStack>
@@ -1289,47 +1123,6 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
     int v = ((lds_int*)stack)[min(max(sp, 0), SCAP - 1) * BS];
     if (take & (sp >= SCAP)) v = ((glb_int*)spill)[(size_t)(sp - SCAP) * stride];
     return v;
-}
-#define spush(stack, spill, sp, e) spush_t<BS>(stack, spill, p.spill_stride, sp, e)
-#define spop(stack, spill, sp) spop_t<BS>(stack, spill, p.spill_stride, sp)
-
-// Visit a 4-wide node: slab-test the four children against (o, inv) with the
-// closest-hit bound `best`; returns the number of hit children and their stack
-// entries nearest first (node: idx << 1; leaf: first << 4 | count << 1 | 1).
-__device__ __forceinline__ int bvh4_visit(const KParams& p, int cur, f3 o, f3 inv, float bound,
-                                          int& e0, int& e1, int& e2, int& e3) {
-    const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
-    const float4 lx = n4[0], hx = n4[1], ly = n4[2], hy = n4[3], lz = n4[4], hz = n4[5];
-    const int4 lk = *reinterpret_cast<const int4*>(n4 + 6);
-    const int4 ct = *reinterpret_cast<const int4*>(n4 + 7);
-    float k[4];
-    int e[4];
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const float lox = c == 0 ? lx.x : c == 1 ? lx.y : c == 2 ? lx.z : lx.w;
-        const float hix = c == 0 ? hx.x : c == 1 ? hx.y : c == 2 ? hx.z : hx.w;
-        const float loy = c == 0 ? ly.x : c == 1 ? ly.y : c == 2 ? ly.z : ly.w;
-        const float hiy = c == 0 ? hy.x : c == 1 ? hy.y : c == 2 ? hy.z : hy.w;
-        const float loz = c == 0 ? lz.x : c == 1 ? lz.y : c == 2 ? lz.z : lz.w;
-        const float hiz = c == 0 ? hz.x : c == 1 ? hz.y : c == 2 ? hz.z : hz.w;
-        const int link = c == 0 ? lk.x : c == 1 ? lk.y : c == 2 ? lk.z : lk.w;
-        const int cnt = c == 0 ? ct.x : c == 1 ? ct.y : c == 2 ? ct.z : ct.w;
-        const float lo[3] = {lox, loy, loz}, hi[3] = {hix, hiy, hiz};
-        float tn, tf;
-        node_slab(lo, hi, o, inv, tn, tf);
-        const bool h = cnt >= 0 && tn <= tf && tf >= -kEps && tn <= bound;
-        k[c] = h ? tn : __int_as_float(0x7f800000);
-        e[c] = cnt == 0 ? (link << 1) : ((link << 4) | (cnt << 1) | 1);
-    }
-    // sort (key, entry) ascending: 5 compare-exchanges
-#define PT_CX(a, b) { const bool sw = k[b] < k[a]; const float tk = sw ? k[b] : k[a]; k[b] = sw ? k[a] : k[b]; k[a] = tk; \
-                      const int te = sw ? e[b] : e[a]; e[b] = sw ? e[a] : e[b]; e[a] = te; }
-    PT_CX(0, 1) PT_CX(2, 3) PT_CX(0, 2) PT_CX(1, 3) PT_CX(1, 2)
-#undef PT_CX
-    const float inf = __int_as_float(0x7f800000);
-    const int n = (k[0] != inf) + (k[1] != inf) + (k[2] != inf) + (k[3] != inf);
-    e0 = e[0]; e1 = e[1]; e2 = e[2]; e3 = e[3];
-    return n;
 }
 
 #ifndef PT_LEAF_STEP
@@ -1378,8 +1171,9 @@ enum {
 };
 constexpr int kContFields = 57;
 
-// F (compile-time variant): 1 = model records in LDS, 2 = leaf triangles as
-// their own steps, 4 = claim source blocks (else: claim slots + search).
+// F (compile-time variant): 1 = model records in LDS, 32 = room for 12 of them
+// (bits 2 and 8 -- leaf triangles as their own steps, phase scheduling -- are
+// always set: the variants without them measured slower and were removed).
 // TAIL: the tail launch, which resumes drain continuations instead of claiming rays.
 template <int BS, int F, bool TAIL = false>
 __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, int bounce, int level) {
@@ -1390,8 +1184,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModels) : 1;
     __shared__ ModelRec s_models[kModelsHere];
     int* stack = s_stack + threadIdx.x;
-    int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
-    int* spill = p.spill + sbase;                        // stack entries beyond the LDS part
+    // (the binary BLAS's depth cap keeps the whole traversal stack in LDS: no spill area)
     // level 0: the main launch; level l >= 1: the tail launch resuming level l - 1's records
     const size_t cfield = (size_t)p.cont_cap * kContFields;        // one record buffer
     const int* cin = p.cont + (size_t)((level - 1) & 1) * cfield;   // records this (tail) launch resumes
@@ -1411,12 +1204,8 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
         __syncthreads();
     }
     const ModelRec* models = lds_models ? s_models : p.models;
-    const int n_prev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
-    const int CH = p.chunk;
-    const int nb = (n_prev + CH - 1) / CH;          // source blocks written by the previous bounce
     const int in_buf = (bounce + 1) & 1;
     const int lane = threadIdx.x & 63;
-    constexpr bool leaf_state = (F & 2) != 0;
     const int n = p.n_live[bounce];
     // lane state: 0 = needs a ray, 1 = select next model, 2 = node visits, 4 = leaf triangles, 3 = no more rays
     int state = 0;
@@ -1425,7 +1214,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     float dlen = 0.0f, gdist = kFMax;
     int gmodel = -1, gtri = -1, im = -1;
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0);
-    int cur = 0, sp = 0, best_tri = -1, n_tris = 0;
+    int cur = 0, sp = 0, best_tri = -1;
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0;    // pending leaves: [lf_i, lf_e) then [lf2_i, lf2_e)
     int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
@@ -1433,7 +1222,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
     unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
-    int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // wave's claimed source block (uniform)
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
@@ -1459,8 +1247,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         cur = C[kCCur * cs]; sp = C[kCSp * cs];
                         lf_i = C[kCLfI * cs]; lf_e = C[kCLfE * cs]; lf2_i = C[kCLf2I * cs]; lf2_e = C[kCLf2E * cs];
                         lf_next = C[kCLfNext * cs];
-                        sbase = C[kCSpill * cs];
-                        spill = p.spill + sbase;
                         best = __int_as_float(C[kCX * cs]); best_tri = C[(kCX + 1) * cs]; any = C[(kCX + 2) * cs] != 0;
 #pragma unroll 1
                         for (int q = 0; q < kStack; q++) stack[q * BS] = C[(kCX + 3 + q) * cs];
@@ -1477,33 +1263,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         state = 3;
                     }
                 }
-            } else if (F & 4) {
-                for (int guard = 0; guard < 4 && idle; guard++) {
-                    if (q_pos >= q_cnt) {                           // claim the next non-empty source block
-                        int b = 0;
-                        if (lane == 0) b = atomicAdd(p.trace_next, 1);
-                        b = __builtin_amdgcn_readlane(b, 0);
-                        if (b >= nb) { exhausted = true; break; }
-                        q_b = b; q_pos = 0; q_cnt = p.blk_cnt[b]; q_off = p.blk_off[b];
-                        continue;
-                    }
-                    const int take = min(__popcll(idle), q_cnt - q_pos);
-                    const int rank = __popcll(idle & ((1ull << lane) - 1ull));
-                    if (state == 0 && rank < take) {
-                        const int src = q_b * CH + q_pos + rank;
-                        j = q_off + q_pos + rank;
-                        const float4 a = p.ray[in_buf][0][kRS * src];
-                        const float4 b = p.ray[in_buf][1][kRS * src];
-                        ow = mk3(a.x, a.y, a.z);
-                        dw = mk3(b.x, b.y, b.z);
-                        winv = node_inv(cull_inv(dw));
-                        dlen = sqrtf(dot(dw, dw));
-                        gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                        state = 1;
-                    }
-                    q_pos += take;
-                    idle = __ballot(state == 0);
-                }
             } else {
                 const int cnt = __popcll(idle);
                 const int leader = __ffsll((long long)idle) - 1;
@@ -1514,17 +1273,11 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 if (state == 0) {
                     j = base + __popcll(idle & ((1ull << lane) - 1ull));
                     if (j < n) {
-                        float4 a, b;
-                        if (p.sray) {                   // the ray copied in claim order: one coalesced 32-B read
-                            a = ld_ray<1>(p.sray + 2 * j); b = ld_ray<1>(p.sray + 2 * j + 1);
-                            j = p.hit_order ? j : __float_as_int(a.w);
-                        } else {
-                            int src;
-                            if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
-                            else src = slot_source(p, j);
-                            a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
-                            b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
-                        }
+                        int src;
+                        if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
+                        else src = slot_source(p, j);
+                        const float4 a = p.ray[in_buf][0][src];
+                        const float4 b = p.ray[in_buf][1][src];
                         ow = mk3(a.x, a.y, a.z);
                         dw = mk3(b.x, b.y, b.z);
                         winv = node_inv(cull_inv(dw));
@@ -1545,13 +1298,13 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
             break;
         }
-        // Phase scheduling (F & 8): one step kind per iteration -- the one most
-        // lanes are waiting in -- so the wave never pays for three partly used blocks.
-        int phase = 7;
-        if (F & 8) {
+        // Phase scheduling: one step kind per iteration -- the one most lanes are
+        // waiting in -- so the wave never pays for three partly used blocks.
+        int phase = 2;
+        {
             const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
                       c4 = __popcll(__ballot(state == 4));
-            phase = 2; int cm = c2;
+            int cm = c2;
             if (c4 * 4 > cm * PT_BVH_LEAF_W) { phase = 4; cm = c4; }
             if (c1 * 4 > cm * PT_BVH_SEL_W) phase = 1;
         }
@@ -1588,7 +1341,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 C[(kCDw + 2) * cs] = __float_as_int(dw.z);
                 C[kCCur * cs] = cur; C[kCSp * cs] = sp;
                 C[kCLfI * cs] = lf_i; C[kCLfE * cs] = lf_e; C[kCLf2I * cs] = lf2_i; C[kCLf2E * cs] = lf2_e;
-                C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = sbase;
+                C[kCLfNext * cs] = lf_next;
                 C[kCX * cs] = __float_as_int(best); C[(kCX + 1) * cs] = best_tri; C[(kCX + 2) * cs] = any ? 1 : 0;
 #pragma unroll 1
                 for (int q = 0; q < kStack; q++) C[(kCX + 3 + q) * cs] = stack[q * BS];
@@ -1599,7 +1352,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             for (;;) {
                 im++;
                 if (im >= p.nmodels) {
-                    put_hit(p, j, gdist, gmodel, gtri, models);
+                    put_hit(p, j, gdist, gmodel, gtri);
                     state = 0;
                     break;
                 }
@@ -1609,7 +1362,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 ninv = node_inv(inv);
-                cur = (F & 16) ? M.bvh4_root : M.bvh_root;
+                cur = M.bvh_root;
                 sp = 0;
                 best = kFMax;
                 best_tri = -1;
@@ -1639,16 +1392,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 }
             }
             lf_i = min(lf_i + PT_LEAF_STEP, lf_e);
-            if ((F & 16) && lf_i == lf_e) {             // 4-wide: everything pending is on the stack
-                if (sp == 0) {
-                    model_done = true;
-                } else {
-                    sp--;
-                    const int e = spop(stack, spill, sp);
-                    if (e & 1) { lf_i = e >> 4; lf_e = lf_i + ((e >> 1) & 7); }
-                    else { cur = e >> 1; state = 2; }
-                }
-            } else if (!(F & 16)) {
+            {
                 // end of the leaf: second leaf child, `next`, or the stack (selects)
                 const bool end = lf_i == lf_e;
                 const bool second = end & (lf2_i < lf2_e);
@@ -1665,30 +1409,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 sp -= pop ? 1 : 0;
             }
         } else if ((phase & 2) && state == 2) {
-            if (F & 16) {
-                // 4-wide node: four slab tests, nearest hit child next, the
-                // others pushed far-to-near (leaves as tagged entries)
-                int e0, e1, e2, e3;
-                const int nhit = bvh4_visit(p, cur, o, ninv, best, e0, e1, e2, e3);
-                if (nhit == 0) {
-                    if (sp == 0) {
-                        model_done = true;
-                    } else {
-                        sp--;
-                        e0 = spop(stack, spill, sp);
-                    }
-                } else {
-                    if (nhit > 3) { spush(stack, spill, sp, e3); sp++; }
-                    if (nhit > 2) { spush(stack, spill, sp, e2); sp++; }
-                    if (nhit > 1) { spush(stack, spill, sp, e1); sp++; }
-                }
-                if (!model_done) {
-                    if (e0 & 1) { lf_i = e0 >> 4; lf_e = lf_i + ((e0 >> 1) & 7); state = 4; }
-                    else cur = e0 >> 1;
-                }
-            } else if (!leaf_state) {
-                model_done = bvh_step<BS>(p, o, d, ninv, cur, sp, stack, best, best_tri, any, n_tris);
-            } else {
+            {
                 // node visit; hit leaf children become pending leaves (tested one
                 // triangle per iteration, in the order bvh_step tests them)
                 const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
@@ -1773,9 +1494,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_WALK_W
 #define PT_WALK_W 8           // k_trace_gf: the walk phase runs when its lanes outnumber the largest other phase's x W/4
 #endif
-#ifndef PT_WALK_DEFER
-#define PT_WALK_DEFER 1       // k_trace_gf: a walk the certificate cannot decide defers its ray to k_trace_deferred
-#endif
 #ifndef PT_LEAF_W
 #define PT_LEAF_W 3           // ... and the leaf phase when they exceed node's x 3/4 (select: x PT_SEL_W/4)
 #endif
@@ -1789,34 +1507,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
-#ifndef PT_CERT_CAP
-#define PT_CERT_CAP PT_GF_HITCAP   // members the main launch's walk certificate handles (walk hand-ons: the rest)
-#endif
-constexpr int kCertCap = PT_CERT_CAP;
-// LDS staging of the top BLAS levels (north_star: "BVH nodes ... staged in LDS").
-// PT_GF_TOP nodes (whole levels: 1, 3, 7 or 15) of one mesh's binary BLAS -- the
-// mesh with the most triangles -- are copied to LDS at kernel start; a node
-// index with kTopFlag set is a slot of that table.  0: off.
-#ifndef PT_GF_TOP
-#define PT_GF_TOP 0
-#endif
-constexpr int kGfTop = PT_GF_TOP;
-// Quantized BLAS for k_trace_gf (verdict r02 item 5a): each binary node's two child
-// boxes as 16-bit planes in its mesh's frame (plane = lo + q * scale, rounded
-// outward), links with the leaf count in the top 5 bits: 32 bytes instead of 64.
-// The slab parameter of a plane is fma(q, A, B) with A = scale / d and
-// B = (lo - o) / d per axis, set once per model; conservative like the float
-// test (the BLAS boxes carry a 1e-4-of-the-diagonal pad, the parameter's
-// rounding is far below it).  0: the float nodes.
-#ifndef PT_GF_QNODES
-#define PT_GF_QNODES 0
-#endif
-constexpr bool kGfQ = PT_GF_QNODES != 0;
-static_assert(!(kGfQ && kGfTop > 0), "PT_GF_QNODES and PT_GF_TOP are exclusive");
-constexpr int kQLinkBits = 27;
-constexpr int kTopFlag = 0x40000000;
-static_assert(kGfTop == 0 || kGfTop == 1 || kGfTop == 3 || kGfTop == 7 || kGfTop == 15, "PT_GF_TOP: whole levels");
-
 // Collection window of k_trace_gf, on voxel boxes instead of the reach R: the
 // walk can enter member h's voxel box before X = t_min + window only if the
 // exact ray enters that box grown by ModelRec::cslack (the DDA's deviation from
@@ -1840,28 +1530,13 @@ __device__ __forceinline__ float vbox_entry(const ModelRec& M, int lo, int hi, f
 }
 __device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3 o, f3 inv, f3 G, float& tn, float& tf,
                                             float& tnx) {
-#if PT_FMA_NODES
     const f3 oi = o * inv;   // hoisted out of the traversal loop by the compiler
     const float a0 = __builtin_fmaf(lo[0], inv.x, -oi.x), b0 = __builtin_fmaf(hi[0], inv.x, -oi.x);
     const float a1 = __builtin_fmaf(lo[1], inv.y, -oi.y), b1 = __builtin_fmaf(hi[1], inv.y, -oi.y);
     const float a2 = __builtin_fmaf(lo[2], inv.z, -oi.z), b2 = __builtin_fmaf(hi[2], inv.z, -oi.z);
-#else
-    const float a0 = (lo[0] - o.x) * inv.x, b0 = (hi[0] - o.x) * inv.x;
-    const float a1 = (lo[1] - o.y) * inv.y, b1 = (hi[1] - o.y) * inv.y;
-    const float a2 = (lo[2] - o.z) * inv.z, b2 = (hi[2] - o.z) * inv.z;
-#endif
     const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
     tn = fmaxf(fmaxf(e0, e1), e2);
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
-    tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
-}
-
-// node_slab_g on slab parameters computed already (quantized nodes): a = entry
-// parameters of the lo planes, b = of the hi planes.
-__device__ __forceinline__ void node_slab_t(const float* a, const float* b, f3 G, float& tn, float& tf, float& tnx) {
-    const float e0 = fminf(a[0], b[0]), e1 = fminf(a[1], b[1]), e2 = fminf(a[2], b[2]);
-    tn = fmaxf(fmaxf(e0, e1), e2);
-    tf = fminf(fminf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fmaxf(a[2], b[2]));
     tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
 }
 
@@ -1872,7 +1547,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     __shared__ int4 s_hs[kGfHitCap * BS];
     constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModelsGf) : 1;
     __shared__ ModelRec s_models[kModelsHere];
-    __shared__ float4 s_top[kGfTop > 0 ? 4 * kGfTop : 1];
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
@@ -1898,12 +1572,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         __syncthreads();
     }
     const ModelRec* models = lds_models ? s_models : p.models;
-    if (kGfTop > 0) {
-        for (int i = threadIdx.x; i < 4 * kGfTop; i += BS) s_top[i] = p.top_nodes[i];
-        __syncthreads();
-    }
-    // the root of model M's collection: the LDS table's slot 0 for the staged mesh
-    auto root_of = [&](const ModelRec& M) { return (kGfTop > 0 && M.mesh == p.top_mesh) ? kTopFlag : M.bvh_root; };
     const int n = p.n_live[bounce];
     const int in_buf = (bounce + 1) & 1;
     const int lane = threadIdx.x & 63;
@@ -1914,19 +1582,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     float gdist = kFMax;
     int gmodel = -1, gtri = -1, im = -1;
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0), G = mk3(0, 0, 0);
-    f3 qA = mk3(0, 0, 0), qB = mk3(0, 0, 0);          // kGfQ: slab parameter = fma(q, qA, qB) per axis
-    auto set_qframe = [&](const ModelRec& M) {
-        if (kGfQ) {
-            const float4 lo = p.qframe[2 * M.mesh], sc = p.qframe[2 * M.mesh + 1];
-            qA = mk3(sc.x * ninv.x, sc.y * ninv.y, sc.z * ninv.z);
-            qB = mk3((lo.x - o.x) * ninv.x, (lo.y - o.y) * ninv.y, (lo.z - o.z) * ninv.z);
-        }
-    };
     float t_box = 0.0f, tmin = kFMax, win = 0.0f;
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
-    int q_b = 0, q_pos = 0, q_cnt = 0, q_off = 0;   // F & 4: the wave's claimed source block (uniform)
-    const int nb_prev = ((bounce == 1 ? p.npix : p.n_live[bounce - 1]) + p.chunk - 1) / p.chunk;
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
     bool exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
@@ -1935,8 +1593,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
-    constexpr bool late = PT_LATE_RAY && !TAIL && !(F & 4) && !kGfQ && kGfTop == 0;
-    bool pend8 = false;                             // late (uniform): lanes in state 8 wait for their ray gather
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
@@ -1983,40 +1639,12 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                         d = normalize(xform12(M.w2m, dw, 0.0f));
                         const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                         ninv = node_inv(inv);
-                        set_qframe(M);
                     }
                 } else {
                     state = 3;
                 }
             }
-        } else if (!TAIL && (F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
-            // claim whole source blocks of the previous bounce: block b's survivors sit at
-            // [b*CH, b*CH + cnt_b) and own dense slots [blk_off[b], blk_off[b] + cnt_b)
-            for (int guard = 0; guard < 4 && idle; guard++) {
-                if (q_pos >= q_cnt) {
-                    int b = 0;
-                    if (lane == 0) b = atomicAdd(p.trace_next, 1);
-                    b = __builtin_amdgcn_readlane(b, 0);
-                    if (b >= nb_prev) { exhausted = true; break; }
-                    q_b = b; q_pos = 0; q_cnt = p.blk_cnt[b]; q_off = p.blk_off[b];
-                    continue;
-                }
-                const int take = min(__popcll(idle), q_cnt - q_pos);
-                const int rank = __popcll(idle & ((1ull << lane) - 1ull));
-                if (state == 0 && rank < take) {
-                    const int src = q_b * p.chunk + q_pos + rank;
-                    j = q_off + q_pos + rank;
-                    const float4 a = p.ray[in_buf][0][kRS * src];
-                    const float4 b = p.ray[in_buf][1][kRS * src];
-                    ow = mk3(a.x, a.y, a.z);
-                    dw = mk3(b.x, b.y, b.z);
-                    gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                    state = 1;
-                }
-                q_pos += take;
-                idle = __ballot(state == 0);
-            }
-        } else if (!TAIL && !(F & 4) && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        } else if (!TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
@@ -2026,35 +1654,20 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (state == 0) {
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
-                    float4 a = make_float4(0, 0, 0, 0), b = a;
-                    if (p.sray) {                   // the ray copied in claim order: one coalesced 32-B read
-                        a = ld_ray<1>(p.sray + 2 * j); b = ld_ray<1>(p.sray + 2 * j + 1);
-                        j = p.hit_order ? j : __float_as_int(a.w);
-                    } else {
-                        int src;
-                        if (p.order) { const int2 e = ld_ord<1>(p.order + j); j = p.hit_order ? j : e.x; src = e.y; }   // sorted claim order
-                        else src = slot_source(p, j);
-                        if (late) {
-                            cur = src;              // the gather waits for the next node step (PT_LATE_RAY)
-                        } else {
-                            a = ld_ray<1>(p.ray[in_buf][0] + kRS * src);
-                            b = ld_ray<1>(p.ray[in_buf][1] + kRS * src);
-                        }
-                    }
+                    int src;
+                    if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
+                    else src = slot_source(p, j);
+                    const float4 a = p.ray[in_buf][0][src];
+                    const float4 b = p.ray[in_buf][1][src];
                     gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
-                    if (late && !p.sray) {
-                        state = 8;
-                    } else {
-                        ow = mk3(a.x, a.y, a.z);
-                        dw = mk3(b.x, b.y, b.z);
-                        state = 1;
-                    }
+                    ow = mk3(a.x, a.y, a.z);
+                    dw = mk3(b.x, b.y, b.z);
+                    state = 1;
                 } else {
                     state = 3;
                 }
             }
         }
-        if (late) pend8 = __ballot(state == 8) != 0;
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
@@ -2063,11 +1676,13 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
             break;
         }
-        int phase = 15;
-        if (F & 8) {
+        // Phase scheduling: one step kind per iteration -- the one most lanes are
+        // waiting in (weighted) -- so the wave never pays for several partly used blocks.
+        int phase = 2;
+        {
             const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
                       c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5));
-            phase = 2; int cm = c2;
+            int cm = c2;
             if (c4 * 4 > cm * PT_LEAF_W) { phase = 4; cm = c4; }
             if (c5 * 4 > cm * PT_WALK_W) { phase = 8; cm = c5; }
             if (c1 * 4 > cm * PT_SEL_W) { phase = 1; cm = c1; }
@@ -2075,16 +1690,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
         phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
-        if (late && pend8 && phase != 2) {            // no node step this iteration: gather now
-            if (state == 8) {
-                const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * cur);
-                const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * cur);
-                ow = mk3(a.x, a.y, a.z);
-                dw = mk3(b.x, b.y, b.z);
-                state = 1;
-            }
-            pend8 = false;
-        }
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
             {
@@ -2106,7 +1711,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             for (;;) {
                 im++;
                 if (im >= p.nmodels) {
-                    put_hit(p, j, gdist, gmodel, gtri, models);
+                    put_hit(p, j, gdist, gmodel, gtri);
                     state = 0;
                     break;
                 }
@@ -2123,14 +1728,13 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                       !((pt.z - M.bbox[2]) < -kEps))) continue;
                 t_box = tb;
                 ninv = node_inv(inv);
-                set_qframe(M);
                 G = mk3((M.vw[0] + M.cslack[0]) * absr(ninv.x), (M.vw[1] + M.cslack[1]) * absr(ninv.y),
                         (M.vw[2] + M.cslack[2]) * absr(ninv.z));
                 if (PT_TRACE_STATS && (p.debug & 512)) G = G * 0.5f;   // timing-only ablation: half-voxel growth
                 if (PT_TRACE_STATS && (p.debug & 1024)) G = mk3(0, 0, 0);   // timing-only ablation: no growth
                 tier = 0;
                 win = (PT_TRACE_STATS && (p.debug & 256)) ? 0.0f : M.wdelta;   // 256: timing-only ablation
-                cur = root_of(M);
+                cur = M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax; pblk = -1;
                 state = 2;
                 break;
@@ -2221,72 +1825,19 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 state = (tonext | pop) ? 2 : state;
                 sp -= pop ? 1 : 0;
             }
-        } else if ((phase & 2) && (state == 2 || (late && pend8 && state == 8))) {   // one node of the collection (window t_min + win)
+        } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
             const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-            const bool nd = !late || state == 2;        // late: state-8 lanes only gather their ray here
-            const int ncur = nd ? cur : 0;
-            float4 q0, q1, q2, q3;
-            if (kGfQ) {
-                // 16-bit planes: child 0 lo.xyz hi.xyz, child 1 lo.xyz hi.xyz; links in w0/w1 of
-                // the second int4.  The decoded slab parameters go straight into q0..q3 in place of
-                // the planes, with an identity ray (o = 0, inv = 1) in node_slab_g below.
-                const int4 a = p.qnodes[2 * cur], b = p.qnodes[2 * cur + 1];
-                auto dq = [](int w, int hi) { return (float)(hi ? ((unsigned)w >> 16) : ((unsigned)w & 0xffffu)); };
-                q0 = make_float4(__builtin_fmaf(dq(a.x, 0), qA.x, qB.x), __builtin_fmaf(dq(a.x, 1), qA.y, qB.y),
-                                 __builtin_fmaf(dq(a.y, 0), qA.z, qB.z), 0.0f);
-                q1 = make_float4(__builtin_fmaf(dq(a.y, 1), qA.x, qB.x), __builtin_fmaf(dq(a.z, 0), qA.y, qB.y),
-                                 __builtin_fmaf(dq(a.z, 1), qA.z, qB.z), 0.0f);
-                q2 = make_float4(__builtin_fmaf(dq(a.w, 0), qA.x, qB.x), __builtin_fmaf(dq(a.w, 1), qA.y, qB.y),
-                                 __builtin_fmaf(dq(b.x, 0), qA.z, qB.z), 0.0f);
-                q3 = make_float4(__builtin_fmaf(dq(b.x, 1), qA.x, qB.x), __builtin_fmaf(dq(b.y, 0), qA.y, qB.y),
-                                 __builtin_fmaf(dq(b.y, 1), qA.z, qB.z), 0.0f);
-                const int lmask = (1 << kQLinkBits) - 1;
-                q0.w = __int_as_float(b.z & lmask);
-                q1.w = __int_as_float(b.w & lmask);
-                q2.w = __int_as_float((int)((unsigned)b.z >> kQLinkBits) - 1);
-                q3.w = __int_as_float((int)((unsigned)b.w >> kQLinkBits) - 1);
-            } else if (kGfTop > 0) {
-                // staged slot: an unconditional LDS read (clamped slot), the global node only for
-                // the lanes below the table (typed pointers keep the two loads apart)
-                typedef float v4f __attribute__((ext_vector_type(4)));
-                typedef __attribute__((address_space(3))) const v4f lds_v4;
-                typedef __attribute__((address_space(1))) const v4f glb_v4;
-                const bool top = (cur & kTopFlag) != 0;
-                const int ti = top ? min(cur & 15, kGfTop - 1) : 0;
-                const lds_v4* t = (const lds_v4*)(s_top + 4 * ti);
-                v4f a0 = t[0], a1 = t[1], a2 = t[2], a3 = t[3];
-                if (!top) {
-                    const glb_v4* g = (const glb_v4*)(nodes + 4 * (size_t)cur);
-                    a0 = g[0]; a1 = g[1]; a2 = g[2]; a3 = g[3];
-                }
-                q0 = make_float4(a0.x, a0.y, a0.z, a0.w); q1 = make_float4(a1.x, a1.y, a1.z, a1.w);
-                q2 = make_float4(a2.x, a2.y, a2.z, a2.w); q3 = make_float4(a3.x, a3.y, a3.z, a3.w);
-            } else {
-                q0 = nodes[4 * ncur + 0];
-                q1 = nodes[4 * ncur + 1];
-                q2 = nodes[4 * ncur + 2];
-                q3 = nodes[4 * ncur + 3];
-            }
-            if (late && !nd) {                          // the refilled lanes' gather, issued after the node loads
-                const float4 a = ld_ray<1>(p.ray[in_buf][0] + kRS * cur);
-                const float4 b = ld_ray<1>(p.ray[in_buf][1] + kRS * cur);
-                ow = mk3(a.x, a.y, a.z);
-                dw = mk3(b.x, b.y, b.z);
-                state = 1;
-            }
-            if (nd) {
+            const float4 q0 = nodes[4 * cur + 0];
+            const float4 q1 = nodes[4 * cur + 1];
+            const float4 q2 = nodes[4 * cur + 2];
+            const float4 q3 = nodes[4 * cur + 3];
             const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
             const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
             const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
             const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
             float tn0, tf0, tn1, tf1, tx0, tx1;
-            if (kGfQ) {                                 // q0..q3 hold slab parameters already
-                node_slab_t(lo0, hi0, G, tn0, tf0, tx0);
-                node_slab_t(lo1, hi1, G, tn1, tf1, tx1);
-            } else {
-                node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
-                node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
-            }
+            node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
+            node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
             const float X = tmin + win;
             const float bound = X + gf_slack(X, t_box);
             // non-short-circuit: both children's slabs in one basic block (a branch on
@@ -2315,9 +1866,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
             lf_next = leaf ? next : lf_next;
             state = leaf ? 4 : state;
-            }
         }
-        if (late) pend8 = false;
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
         if (collected) {
             if (nh > 0) {
@@ -2330,7 +1879,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 const ModelRec& M = models[im];
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = root_of(M);
+                cur = M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2344,24 +1893,14 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (PT_TRACE_STATS && (p.debug & 128) && pblk < 0) {      // timing-only ablation: no walk at all
                 w.hit = true; w.has_best = true; w.final_min = true; w.t = tmin; w.tri = -1; w.tw = 0.0f;
                 for (int h = 0; h < nh; h++) if (__int_as_float(hs[h * BS].x) == tmin) w.tri = hs[h * BS].y;
-            } else if (!TAIL && !(F & 16) && PT_WALK_DEFER) {
+            } else if (!TAIL && !(F & 16)) {
                 // the certificate only; a ray it cannot decide is handed on to the tail launch
                 // (which walks it exactly) or, past the records' room, to k_trace_deferred
                 int tri = -1;
-                bool ok;
-                if (kCertCap < kGfHitCap) {
-                    // the main launch certifies hit sets of at most kCertCap members (97 % of the
-                    // walks at configs[1]: 18 % one member, 79 % two -- a slab's two faces in one
-                    // voxel); larger ones and pool hit sets go to the tail launch with the rest
-                    const bool small = pblk < 0 && nh <= kCertCap;
-                    ok = small && walk_certify<kCertCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; },
-                                                         nh, tmin, win, tri);
-                } else {
-                    const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
-                    ok = pblk < 0
-                        ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
-                        : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
-                }
+                const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
+                const bool ok = pblk < 0
+                    ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
+                    : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
                 if (!ok) state = 6;
             } else {
@@ -2380,7 +1919,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             } else {                                    // not provably exact: next tier's collection
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = root_of(M);
+                cur = M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2464,15 +2003,15 @@ __global__ __launch_bounds__(BS) void k_trace_deferred(KParams p, int bounce) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && cnt > 0)      // every build: which route the rays took
         atomicAdd(p.segments + kDeferredRayCounter, (unsigned long long)cnt);
     for (int q = blockIdx.x * BS + threadIdx.x; q < cnt; q += gridDim.x * BS) {
-        const int j = p.defer_slots[q];              // hit_order: the claim position
-        const int src = p.hit_order ? p.order[j].y : slot_source(p, j);
-        const float4 a = p.ray[in_buf][0][kRS * src];
-        const float4 b = p.ray[in_buf][1][kRS * src];
+        const int j = p.defer_slots[q];
+        const int src = slot_source(p, j);
+        const float4 a = p.ray[in_buf][0][src];
+        const float4 b = p.ray[in_buf][1][src];
         float gdist;
         int gmodel, gtri;
         intersect_scene_g<ACCEL_GRID_FAST, BS>(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), s_stack + threadIdx.x,
                                                s_hs + threadIdx.x, gdist, gmodel, gtri);
-        put_hit(p, j, gdist, gmodel, gtri, p.models);
+        put_hit(p, j, gdist, gmodel, gtri);
     }
 }
 
@@ -2487,13 +2026,7 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
     // them so XCD x processes the contiguous chunk range [x q, (x+1) q) of the live
     // pool -- neighbouring rays (neighbouring pixels' paths) share one L2.  The grid
     // has nblocks + 8 workgroups so the permutation covers every live chunk.
-    int chunk = blockIdx.x;
-    if (PT_XCD_MAP) {
-        const int nact = (n + BS - 1) / BS;
-        const int q = (nact + 7) >> 3;
-        chunk = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
-        if ((int)(blockIdx.x >> 3) >= q) chunk = 0x7fffffff;
-    }
+    const int chunk = blockIdx.x;
     const int j0 = chunk >= (n + BS - 1) / BS ? n : chunk * BS;
     if (j0 >= n) return;                       // whole block idle (uniform)
     const int j = j0 + threadIdx.x;
@@ -2514,26 +2047,20 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
             h.model = p.cache_model[j];
         } else {
             // dense slot j -> (source block b, rank) via the scan of the previous bounce
-            int src;
-            if (p.use_slotmap) {
-                src = p.slot_src[j];
-            } else {
-                int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
-                }
-                src = lo * BS + (j - p.blk_off[lo]);
+            int lo = p.dst_start[chunk], hi = p.dst_start[chunk + 1];
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (p.blk_off[mid] <= j) lo = mid; else hi = mid - 1;
             }
-            const float4 a = ld_ray<2>(p.ray[in_buf][0] + kRS * src);
-            const float4 b = ld_ray<2>(p.ray[in_buf][1] + kRS * src);
-            const float4 c = ld_ray<2>(p.ray[in_buf][2] + src);
+            const int src = lo * BS + (j - p.blk_off[lo]);
+            const float4 a = p.ray[in_buf][0][src];
+            const float4 b = p.ray[in_buf][1][src];
+            const float4 c = p.ray[in_buf][2][src];
             r.o = mk3(a.x, a.y, a.z); r.pixel = __float_as_int(a.w);
             r.d = mk3(b.x, b.y, b.z); r.bounces = __float_as_int(b.w);
             r.c = mk3(c.x, c.y, c.z);
             if (ACCEL == kAccelHitBuffer) {       // traced by k_trace_bvh / k_trace_gf
-                const int hj = p.hit_order ? p.slot_pos[j] : j;   // hit_order: records sit in claim order
-                h = get_hit(p, hj);
+                h = get_hit(p, j);
             } else {
                 h = intersect_scene<ACCEL, BS>(p, r.o, r.d, s_stack + threadIdx.x, s_hs + threadIdx.x);
             }
@@ -2578,9 +2105,9 @@ __global__ __launch_bounds__(BS, (ACCEL == ACCEL_GRID_FAST && !FIRST) ? 3 : PT_M
     }
     if (alive) {
         const int dst = j0 + base + rank;
-        st_ray<2>(p.ray[out_buf][0] + kRS * dst, make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(r.pixel)));
-        st_ray<2>(p.ray[out_buf][1] + kRS * dst, make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(r.bounces)));
-        st_ray<2>(p.ray[out_buf][2] + dst, make_float4(r.c.x, r.c.y, r.c.z, 0.0f));
+        p.ray[out_buf][0][dst] = make_float4(r.o.x, r.o.y, r.o.z, __int_as_float(r.pixel));
+        p.ray[out_buf][1][dst] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(r.bounces));
+        p.ray[out_buf][2][dst] = make_float4(r.c.x, r.c.y, r.c.z, 0.0f);
     }
     if (threadIdx.x == 0) p.blk_cnt[chunk] = total;
 }
@@ -2653,17 +2180,6 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
         for (int i = tid; i < 2 * kSortBins; i += kScanWG) p.sort_bins[i] = 0;
 }
 
-// Slot map for bounce+1: dense slot blk_off[b] + r <- source index b * chunk + r
-// (block b's r-th survivor), so readers of slot j need one load, not a search.
-__global__ __launch_bounds__(256) void k_slotmap(KParams p, int bounce) {
-    const int n = bounce == 0 ? p.npix : p.n_live[bounce];
-    const int CH = p.chunk;
-    const int i = blockIdx.x * 256 + threadIdx.x;   // source index
-    if (i >= ((n + CH - 1) / CH) * CH) return;
-    const int b = i / CH, r = i - b * CH;
-    if (r < p.blk_cnt[b]) p.slot_src[p.blk_off[b] + r] = i;
-}
-
 // ---------------------------------------------------------------------------
 // Ray sort before a persistent trace (bounce >= 1).  The trace result of a ray
 // does not depend on which lane traces it or when, so the claim order is free:
@@ -2713,21 +2229,6 @@ __device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
                    (((a >> 2) & 1) << 5) | (((b >> 2) & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) |
                    ((a & 1) << 1) | (b & 1);
         }
-        case 9: { // 14 bits, interleaved, origin 4^3 and direction 16 x 16: u3 v3 x1 y1 z1 u2 v2 x0 y0 z0 u1 v1 u0 v0
-            const int a = iu >> 2, b = iv >> 2, x = ix >> 2, y = iy >> 2, z = iz >> 2;
-            return (((a >> 3) & 1) << 13) | (((b >> 3) & 1) << 12) | (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) |
-                   (((z >> 1) & 1) << 9) | (((a >> 2) & 1) << 8) | (((b >> 2) & 1) << 7) | ((x & 1) << 6) |
-                   ((y & 1) << 5) | ((z & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) |
-                   ((a & 1) << 1) | (b & 1);
-        }
-        case 10: { // 15 bits, interleaved, origin 8^3 and direction 8 x 8: x2 y2 z2 u2 v2 x1 y1 z1 u1 v1 x0 y0 z0 u0 v0
-            const int a = iu >> 3, b = iv >> 3, x = ix >> 1, y = iy >> 1, z = iz >> 1;
-            int m = 0;
-            for (int q = 2; q >= 0; q--)
-                m = (m << 5) | (((x >> q) & 1) << 4) | (((y >> q) & 1) << 3) | (((z >> q) & 1) << 2) |
-                    (((a >> q) & 1) << 1) | ((b >> q) & 1);
-            return m;
-        }
         default: { // interleaved: u2 v2 x1 y1 z1 u1 v1 x0 y0 z0 u0 v0 (u, v: 3 bits, x, y, z: 2 bits)
             const int a = iu >> 3, b = iv >> 3, x = ix >> 2, y = iy >> 2, z = iz >> 2;
             return (((a >> 2) & 1) << 11) | (((b >> 2) & 1) << 10) | (((x >> 1) & 1) << 9) | (((y >> 1) & 1) << 8) |
@@ -2754,8 +2255,8 @@ __global__ __launch_bounds__(kSortWG) void k_sort_hist(KParams p, int bounce) {
         if (i < lim) {
             const int c = i / p.chunk, r = i - c * p.chunk;
             if (r < p.blk_cnt[c]) {
-                const float4 a = ld_ray<4>(p.ray[in_buf][0] + kRS * i);
-                const float4 b = ld_ray<4>(p.ray[in_buf][1] + kRS * i);
+                const float4 a = p.ray[in_buf][0][i];
+                const float4 b = p.ray[in_buf][1][i];
                 const int key = sort_key(p, mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z));
                 p.sort_key[i] = (unsigned short)key;
                 atomicAdd(&s_h[key], 1);
@@ -2791,7 +2292,6 @@ __global__ __launch_bounds__(kSortWG) void k_sort_prefix(KParams p) {
 
 __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce) {
     __shared__ int s_h[kSortBins];                       // local counts, then this workgroup's base per key
-    const int in_buf = (bounce + 1) & 1;
     const int nprev = bounce == 1 ? p.npix : p.n_live[bounce - 1];
     const int lim = ((nprev + p.chunk - 1) / p.chunk) * p.chunk;
     const int i0 = blockIdx.x * (kSortWG * kSortPer);
@@ -2824,14 +2324,6 @@ __global__ __launch_bounds__(kSortWG) void k_sort_scatter(KParams p, int bounce)
         if (key[t] >= 0) {
             const int pos = s_h[key[t]] + rank[t];
             p.order[pos] = make_int2(jj[t], i0 + t * kSortWG + tid);
-            if (p.sray) {                                // PT_SORT_COPY: the ray itself, in claim order
-                const int i = i0 + t * kSortWG + tid;
-                const float4 a = ld_ray<4>(p.ray[in_buf][0] + kRS * i);
-                const float4 b = ld_ray<4>(p.ray[in_buf][1] + kRS * i);
-                p.sray[2 * pos] = make_float4(a.x, a.y, a.z, __int_as_float(jj[t]));
-                p.sray[2 * pos + 1] = b;
-            }
-            if (p.hit_order) p.slot_pos[jj[t]] = pos;
         }
 }
 
@@ -2952,7 +2444,6 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
-    PT_HIP(upload(allocs, &kp.bvh4, scene.bvh4_nodes.data(), scene.bvh4_nodes.size() * sizeof(Bvh4Node), stream));
 
     kp.width = cfg.width;
     kp.height = cfg.height;
@@ -2986,8 +2477,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         split_trace = cfg.accel == ACCEL_BVH && !(e && std::atoi(e) == 0);
         const char* eg = std::getenv("PT_GF_SPLIT");
         if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
+        // trace variants: 9 / 11 model records in LDS (the default), 8 / 10 from global memory
         const char* gff = std::getenv("PT_GF_FLAGS");
         gf_flags = gff ? std::atoi(gff) : 9;
+        if (gf_flags != 8 && gf_flags != 9) { last_error = "PT_GF_FLAGS must be 8 or 9"; return -1; }
         // 9..12 instances: the default variants with room for 12 LDS model records (F | 32)
         gf_wide_lds = (gf_flags & ~1) == 8 && (gf_flags & 1) && scene.model_recs.size() > (size_t)kLdsModelsGf &&
                       scene.model_recs.size() <= (size_t)kLdsModelsWide;
@@ -2996,8 +2489,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
         kp.trace_flags = tf ? std::atoi(tf) : 11;
+        if (kp.trace_flags != 10 && kp.trace_flags != 11) { last_error = "PT_TRACE_FLAGS must be 10 or 11"; return -1; }
         // the default variant with 9..12 models: model records in LDS with room for 12 (F | 32)
-        bvh_wide_lds = (kp.trace_flags & 31) == 11 && scene.model_recs.size() > (size_t)kLdsModels &&
+        bvh_wide_lds = kp.trace_flags == 11 && scene.model_recs.size() > (size_t)kLdsModels &&
                        scene.model_recs.size() <= (size_t)kLdsModelsWide;
         if (scene.model_recs.size() > (size_t)kLdsModels) kp.trace_flags &= ~1;
         int dev = 0, cus = 256;
@@ -3011,17 +2505,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
         const int w = wpc ? std::max(1, std::atoi(wpc)) : (npipes > 1 ? 8 : 20);
         trace_blocks = std::max(1, cus) * w;
-        // 4-wide traversal pushes up to 3 entries per level: LDS holds kStack, the rest spills
-        if (split_trace && (kp.trace_flags & 16) && 3 * scene.bvh4_max_depth > kStack + kSpillEntries) {
-            last_error = "BVH4 too deep for the traversal stack";
-            return -1;
-        }
-        const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (kp.trace_flags & 16));
-        // drain continuations (default variants only: gf flags 9 / 8, bvh flags 11 / 10)
+        const bool spills = split_trace && cfg.accel == ACCEL_GRID_FAST;   // k_trace_gf's 12-entry LDS stack
+        // drain continuations
         const char* dd = std::getenv("PT_DRAIN_DUMP");
-        const bool def_variant = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & ~1) == 8
-                                                              : ((kp.trace_flags & ~1) == 10 || (kp.trace_flags & ~1) == 26);
-        kp.drain_dump = split_trace && def_variant ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
+        kp.drain_dump = split_trace ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
         // walk hand-ons (k_trace_gf main launch -> its level-1 tail): room for one per lane
         // (PT_WALK_WCAP overrides; beyond it a ray goes whole to k_trace_deferred).  With one
@@ -3031,30 +2518,16 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* wh = std::getenv("PT_WALK_HANDON");
         const char* wc = std::getenv("PT_WALK_WCAP");
         const bool handon = wh ? std::atoi(wh) != 0 : npipes > 1;
-        kp.cont_wcap = split_trace && cfg.accel == ACCEL_GRID_FAST && (gf_flags & ~1) == 8 && handon
+        kp.cont_wcap = split_trace && cfg.accel == ACCEL_GRID_FAST && handon
                            ? (wc ? std::max(0, std::atoi(wc)) : trace_blocks * 64) : 0;
         const char* dl = std::getenv("PT_DRAIN_LEVELS");     // tail launches; the last one runs to the end
         kp.drain_levels = std::max(1, std::min(kDrainLevels, dl ? std::atoi(dl) : 1));
         kp.spill_stride = spills ? 2 * trace_blocks * 64 : 1;   // main lanes, then tail lanes' own areas
-        const char* sm = std::getenv("PT_SLOTMAP");
-        kp.use_slotmap = sm ? (std::atoi(sm) != 0) : 0;   // measured neutral (binary search is not the refill cost)
         // Ray sort before each persistent trace (claim order only; results unchanged).
         const char* so = std::getenv("PT_SORT");
-        const bool block_claims = cfg.accel == ACCEL_GRID_FAST ? (gf_flags & 4) : (kp.trace_flags & 4);
         // auto: key 7 for both persistent traces (bvh: 3421 -> 3571 Mrays/s at 8 waves per CU, 16 pipelines)
         const int want = so ? std::atoi(so) : cfg.ray_sort >= 0 ? cfg.ray_sort : 7;
-        // keys 9 (14 bits) and 10 (15 bits) need a PT_SORT_BITS build that wide
-        const int max_key = kSortBits >= 15 ? 10 : kSortBits >= 14 ? 9 : 8;
-        kp.sort_mode = (split_trace && !block_claims) ? std::max(0, std::min(max_key, want)) : 0;
-        // PT_HIT_ORDER=1: the traces write hit records at the ray's claim position (rays claimed
-        // together finish close in time, so their records share L2 lines before write-back); the
-        // shading pass finds slot j's record through slot_pos[j].  Results identical.
-        const char* ho = std::getenv("PT_HIT_ORDER");
-        kp.hit_order = kp.sort_mode && ho && std::atoi(ho) != 0;
-        // PT_SORT_COPY=1: the scatter copies each ray to its claim position, so a trace refill
-        // reads (ray, slot) in one coalesced load instead of the order entry and then the ray
-        const char* sc = std::getenv("PT_SORT_COPY");
-        kp.sort_copy = kp.sort_mode && (sc ? std::atoi(sc) != 0 : kSortCopyDefault);
+        kp.sort_mode = split_trace ? std::max(0, std::min(8, want)) : 0;
         float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
         for (const ModelRec& m : scene.model_recs)
             for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], m.wbox[a]); hi[a] = std::max(hi[a], m.wbox[3 + a]); }
@@ -3064,111 +2537,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
             kp.sort_sc[a] = ext > 0.0f && ext < 1e30f ? 16.0f / ext : 0.0f;
         }
     }
-    kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr; kp.sray = nullptr;
-    kp.top_nodes = nullptr;
-    kp.top_mesh = -1;
-    kp.qnodes = nullptr;
-    kp.qframe = nullptr;
-    if (kGfQ && cfg.accel == ACCEL_GRID_FAST) {
-        // 32-byte quantized copy of the binary BLAS (same node indices), per mesh frame
-        const size_t nn = scene.bvh_nodes.size();
-        std::vector<int4> q(2 * nn, make_int4(0, 0, 0, 0));
-        std::vector<float4> frame(2 * scene.meshes.size(), make_float4(0, 0, 0, 0));
-        for (size_t m = 0; m < scene.meshes.size(); m++) {
-            const int root = scene.mesh_bvh_root[m];
-            if (root < 0) continue;
-            std::vector<int> order{root};
-            double flo[3] = {1e300, 1e300, 1e300}, fhi[3] = {-1e300, -1e300, -1e300};
-            for (size_t i = 0; i < order.size(); i++) {
-                const BvhNode& nd = scene.bvh_nodes[order[i]];
-                const int cnt[2] = {nd.count0, nd.count1};
-                const float* lo[2] = {nd.lo0, nd.lo1};
-                const float* hi[2] = {nd.hi0, nd.hi1};
-                for (int c = 0; c < 2; c++) {
-                    if (cnt[c] < 0) continue;
-                    for (int k = 0; k < 3; k++) { flo[k] = std::min(flo[k], (double)lo[c][k]); fhi[k] = std::max(fhi[k], (double)hi[c][k]); }
-                }
-                if (nd.count0 == 0) order.push_back(nd.link0);
-                if (nd.count1 == 0) order.push_back(nd.link1);
-            }
-            float fl[3], sc[3];
-            for (int k = 0; k < 3; k++) {
-                if (!(flo[k] <= fhi[k]) || !std::isfinite(flo[k]) || !std::isfinite(fhi[k])) {
-                    last_error = "quantized BLAS: mesh box not finite";
-                    return -1;
-                }
-                fl[k] = (float)flo[k];
-                if ((double)fl[k] > flo[k]) fl[k] = std::nextafter(fl[k], -INFINITY);
-                sc[k] = (float)std::max((fhi[k] - (double)fl[k]) / 65535.0, 1e-30);
-                while ((double)fl[k] + 65535.0 * (double)sc[k] < fhi[k]) sc[k] = std::nextafter(sc[k], INFINITY);
-            }
-            frame[2 * m] = make_float4(fl[0], fl[1], fl[2], 0.0f);
-            frame[2 * m + 1] = make_float4(sc[0], sc[1], sc[2], 0.0f);
-            auto qlo = [&](float v, int k) {
-                double x = std::floor(((double)v - fl[k]) / sc[k]);
-                x = std::min(std::max(x, 0.0), 65535.0);
-                while (x > 0 && (double)fl[k] + x * (double)sc[k] > (double)v) x -= 1.0;
-                return (unsigned)x;
-            };
-            auto qhi = [&](float v, int k) {
-                double x = std::ceil(((double)v - fl[k]) / sc[k]);
-                x = std::min(std::max(x, 0.0), 65535.0);
-                while (x < 65535.0 && (double)fl[k] + x * (double)sc[k] < (double)v) x += 1.0;
-                return (unsigned)x;
-            };
-            for (int n : order) {
-                const BvhNode& nd = scene.bvh_nodes[n];
-                unsigned w[6] = {0, 0, 0, 0, 0, 0};
-                const int cnt[2] = {nd.count0, nd.count1};
-                const int link[2] = {nd.link0, nd.link1};
-                const float* lo[2] = {nd.lo0, nd.lo1};
-                const float* hi[2] = {nd.hi0, nd.hi1};
-                unsigned v[12];
-                for (int c = 0; c < 2; c++)
-                    for (int k = 0; k < 3; k++) {
-                        v[6 * c + k] = cnt[c] >= 0 ? qlo(lo[c][k], k) : 1;
-                        v[6 * c + 3 + k] = cnt[c] >= 0 ? qhi(hi[c][k], k) : 0;
-                    }
-                for (int i = 0; i < 6; i++) w[i] = v[2 * i] | (v[2 * i + 1] << 16);
-                int lw[2];
-                for (int c = 0; c < 2; c++) {
-                    if (cnt[c] + 1 >= 32 || (cnt[c] >= 0 && (link[c] < 0 || link[c] >= (1 << kQLinkBits)))) {
-                        last_error = "quantized BLAS: link or leaf count out of range";
-                        return -1;
-                    }
-                    lw[c] = (cnt[c] < 0 ? 0 : link[c]) | ((cnt[c] + 1) << kQLinkBits);
-                }
-                q[2 * (size_t)n] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
-                q[2 * (size_t)n + 1] = make_int4((int)w[4], (int)w[5], lw[0], lw[1]);
-            }
-        }
-        PT_HIP(upload(allocs, &kp.qnodes, q.data(), q.size() * sizeof(int4), stream));
-        PT_HIP(upload(allocs, &kp.qframe, frame.data(), frame.size() * sizeof(float4), stream));
-    }
-    if (kGfTop > 0 && cfg.accel == ACCEL_GRID_FAST) {
-        // k_trace_gf's LDS table: the first kGfTop nodes, breadth first, of the BLAS of the
-        // mesh with the most triangles; inner links into the table become kTopFlag | slot
-        long long most = -1;
-        for (const ModelRec& m : scene.model_recs)
-            if ((long long)m.tri_end - m.tri_start > most) { most = (long long)m.tri_end - m.tri_start; kp.top_mesh = m.mesh; }
-        std::vector<BvhNode> top(kGfTop);
-        std::memset(top.data(), 0, top.size() * sizeof(BvhNode));
-        std::vector<int> gid{scene.mesh_bvh_root[kp.top_mesh]};
-        for (size_t i = 0; i < gid.size(); i++) {
-            const BvhNode& nd = scene.bvh_nodes[gid[i]];
-            if (nd.count0 == 0 && (int)gid.size() < kGfTop) gid.push_back(nd.link0);
-            if (nd.count1 == 0 && (int)gid.size() < kGfTop) gid.push_back(nd.link1);
-        }
-        for (size_t i = 0; i < gid.size(); i++) {
-            BvhNode nd = scene.bvh_nodes[gid[i]];
-            for (size_t k = 1; k < gid.size(); k++) {
-                if (nd.count0 == 0 && nd.link0 == gid[k]) nd.link0 = kTopFlag | (int)k;
-                if (nd.count1 == 0 && nd.link1 == gid[k]) nd.link1 = kTopFlag | (int)k;
-            }
-            top[i] = nd;
-        }
-        PT_HIP(upload(allocs, &kp.top_nodes, top.data(), top.size() * sizeof(BvhNode), stream));
-    }
+    kp.order = nullptr; kp.sort_bins = nullptr; kp.sort_key = nullptr;
     PT_HIP(upload(allocs, &kp.segments, nullptr, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     PT_HIP(hipMemsetAsync(kp.segments, 0, (kDiagCounters + kMaxBounceCounters) * sizeof(unsigned long long), stream));
     // Pipelines: iterations in flight on their own streams, each with its own
@@ -3210,10 +2579,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
 // spill, hit buffer and work counters.
 int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     for (int b = 0; b < 2; b++)
-        for (int q = 0; q < 3; q++) {
-            if (q == 1 && kRS == 2) { k.ray[b][1] = k.ray[b][0] + 1; continue; }   // interleaved with plane 0
-            PT_HIP(upload(allocs, &k.ray[b][q], nullptr, (q < 2 ? kRS : 1) * cap * sizeof(float4), st));
-        }
+        for (int q = 0; q < 3; q++) PT_HIP(upload(allocs, &k.ray[b][q], nullptr, cap * sizeof(float4), st));
     PT_HIP(upload(allocs, &k.blk_cnt, nullptr, (k.nblocks + 1) * sizeof(int), st));
     PT_HIP(upload(allocs, &k.blk_off, nullptr, (k.nblocks + 2) * sizeof(int), st));
     PT_HIP(upload(allocs, &k.dst_start, nullptr, (k.nblocks + 2) * sizeof(int), st));
@@ -3227,13 +2593,10 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(upload(allocs, &k.defer_slots, nullptr, dcap * sizeof(int), st));
     PT_HIP(upload(allocs, &k.defer_count, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.defer_count, 0, sizeof(int), st));
-    PT_HIP(upload(allocs, &k.slot_src, nullptr, (k.use_slotmap ? cap : 1) * sizeof(int), st));
     if (k.sort_mode) {
         PT_HIP(upload(allocs, &k.order, nullptr, cap * sizeof(int2), st));
         PT_HIP(upload(allocs, &k.sort_key, nullptr, cap * sizeof(unsigned short), st));
         PT_HIP(upload(allocs, &k.sort_bins, nullptr, 2 * kSortBins * sizeof(int), st));
-        PT_HIP(upload(allocs, &k.slot_pos, nullptr, (k.hit_order ? cap : 1) * sizeof(int), st));
-        if (k.sort_copy) PT_HIP(upload(allocs, &k.sray, nullptr, 2 * cap * sizeof(float4), st));
         PT_HIP(hipMemsetAsync(k.sort_bins, 0, 2 * kSortBins * sizeof(int), st));
     }
     const size_t hcap = split_trace ? cap : 1;
@@ -3279,27 +2642,20 @@ int Renderer::launchPrimary() {
 void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
     const dim3 g((unsigned)trace_blocks), t(64);
     if (cfg.accel == ACCEL_GRID_FAST) {
-        // model records in LDS: the variant asks for them (gf_flags & 1, cleared by
-        // allocateOnGPU when the scene has more models than the tables hold)
+        // model records in LDS (gf_flags & 1, cleared by allocateOnGPU when the scene has
+        // more models than the tables hold); 9..12 models: the 12-record variants (F | 32).
+        // With walk hand-ons the main launch only certifies (F = 9 / 41 / 8), else (F | 16)
+        // it walks in place.
         const bool lds = (gf_flags & 1) && k.nmodels <= kLdsModelsGf;
-        const bool wide = gf_wide_lds;                  // 9..12 models: the 12-record variants
-        switch (gf_flags) {
-            case 0: hipLaunchKernelGGL((k_trace_gf<64, 0>), g, t, 0, st, k, b, 0); break;
-            case 1: hipLaunchKernelGGL((k_trace_gf<64, 1>), g, t, 0, st, k, b, 0); break;
-            case 12: hipLaunchKernelGGL((k_trace_gf<64, 12>), g, t, 0, st, k, b, 0); break;
-            case 13: hipLaunchKernelGGL((k_trace_gf<64, 13>), g, t, 0, st, k, b, 0); break;
-            default:                         // 9 and 8 (more models than LDS holds): certificate-only main
-                                             // launch with walk hand-ons, else (| 16) walks in place
-                if (k.cont_wcap > 0) {
-                    if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
-                    else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 41>), g, t, 0, st, k, b, 0);
-                    else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
-                } else {
-                    if (lds) hipLaunchKernelGGL((k_trace_gf<64, 25>), g, t, 0, st, k, b, 0);
-                    else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 57>), g, t, 0, st, k, b, 0);
-                    else hipLaunchKernelGGL((k_trace_gf<64, 24>), g, t, 0, st, k, b, 0);
-                }
-                break;
+        const bool wide = gf_wide_lds;
+        if (k.cont_wcap > 0) {
+            if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9>), g, t, 0, st, k, b, 0);
+            else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 41>), g, t, 0, st, k, b, 0);
+            else hipLaunchKernelGGL((k_trace_gf<64, 8>), g, t, 0, st, k, b, 0);
+        } else {
+            if (lds) hipLaunchKernelGGL((k_trace_gf<64, 25>), g, t, 0, st, k, b, 0);
+            else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 57>), g, t, 0, st, k, b, 0);
+            else hipLaunchKernelGGL((k_trace_gf<64, 24>), g, t, 0, st, k, b, 0);
         }
         for (int l = 1; (k.drain_dump > 0 && l <= k.drain_levels) || (k.cont_wcap > 0 && l == 1); l++) {
             // the rays handed on (drain continuations; walk hand-ons go to level 1), packed
@@ -3311,34 +2667,17 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
         hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, PT_DEFER_WGS)), t, 0, st, k, b);
         return;
     }
-    switch (bvh_wide_lds ? 43 : (k.trace_flags & 31)) {
-        case 43: hipLaunchKernelGGL((k_trace_bvh<64, 43>), g, t, 0, st, k, b, 0); break;   // 11 with 9..12 models
-        case 0: hipLaunchKernelGGL((k_trace_bvh<64, 0>), g, t, 0, st, k, b, 0); break;
-        case 1: hipLaunchKernelGGL((k_trace_bvh<64, 1>), g, t, 0, st, k, b, 0); break;
-        case 2: hipLaunchKernelGGL((k_trace_bvh<64, 2>), g, t, 0, st, k, b, 0); break;
-        case 3: hipLaunchKernelGGL((k_trace_bvh<64, 3>), g, t, 0, st, k, b, 0); break;
-        case 4: hipLaunchKernelGGL((k_trace_bvh<64, 4>), g, t, 0, st, k, b, 0); break;
-        case 5: hipLaunchKernelGGL((k_trace_bvh<64, 5>), g, t, 0, st, k, b, 0); break;
-        case 6: hipLaunchKernelGGL((k_trace_bvh<64, 6>), g, t, 0, st, k, b, 0); break;
-        case 7: hipLaunchKernelGGL((k_trace_bvh<64, 7>), g, t, 0, st, k, b, 0); break;
-        case 10: hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b, 0); break;
-        case 26: hipLaunchKernelGGL((k_trace_bvh<64, 26>), g, t, 0, st, k, b, 0); break;
-        case 27: hipLaunchKernelGGL((k_trace_bvh<64, 27>), g, t, 0, st, k, b, 0); break;
-        case 18: hipLaunchKernelGGL((k_trace_bvh<64, 18>), g, t, 0, st, k, b, 0); break;
-        case 19: hipLaunchKernelGGL((k_trace_bvh<64, 19>), g, t, 0, st, k, b, 0); break;
-        default:                             // 11; 10 when the model records do not fit LDS
-            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b, 0);
-            else hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b, 0);
-            break;
-    }
-    const bool wide = (k.trace_flags & 16) != 0;
-    for (int l = 1; k.drain_dump > 0 && l <= k.drain_levels; l++) {       // the rays handed on, packed
-        if (wide) {
-            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 27, true>), g, t, 0, st, k, b, l);
-            else hipLaunchKernelGGL((k_trace_bvh<64, 26, true>), g, t, 0, st, k, b, l);
+    // k_trace_bvh: 11 (LDS records), 43 (11 with room for 12), 10 (records in global memory)
+    const bool lds = k.trace_flags == 11 && k.nmodels <= kLdsModels;
+    for (int l = 0; l == 0 || (k.drain_dump > 0 && l <= k.drain_levels); l++) {   // main launch, then the tails
+        if (bvh_wide_lds) {
+            if (l == 0) hipLaunchKernelGGL((k_trace_bvh<64, 43>), g, t, 0, st, k, b, 0);
+            else hipLaunchKernelGGL((k_trace_bvh<64, 43, true>), g, t, 0, st, k, b, l);
+        } else if (lds) {
+            if (l == 0) hipLaunchKernelGGL((k_trace_bvh<64, 11>), g, t, 0, st, k, b, 0);
+            else hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b, l);
         } else {
-            if (k.nmodels <= kLdsModels) hipLaunchKernelGGL((k_trace_bvh<64, 11, true>), g, t, 0, st, k, b, l);
-            else if (bvh_wide_lds) hipLaunchKernelGGL((k_trace_bvh<64, 43, true>), g, t, 0, st, k, b, l);
+            if (l == 0) hipLaunchKernelGGL((k_trace_bvh<64, 10>), g, t, 0, st, k, b, 0);
             else hipLaunchKernelGGL((k_trace_bvh<64, 10, true>), g, t, 0, st, k, b, l);
         }
     }
@@ -3414,10 +2753,6 @@ int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
         if (pall) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, st); }
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanWG), 0, st, k, b);
         PT_HIP(hipGetLastError());
-        if (k.use_slotmap && b + 1 < passes) {
-            hipLaunchKernelGGL(k_slotmap, dim3((unsigned)((k.nblocks * k.chunk + 255) / 256)), dim3(256), 0, st, k, b);
-            PT_HIP(hipGetLastError());
-        }
         if (pall) { hipEventRecord(e1, st); scan_events.push_back({e0, e1}); }
     }
     return 0;

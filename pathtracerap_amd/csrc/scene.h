@@ -95,9 +95,6 @@ public:
                                       // the triangle index and its packed grid voxel box (mn, mx; 10 bits/axis)
     std::vector<int> tri_vbox;        // 2 ints / triangle: packed computeVoxelIndex min / max
     std::vector<int> mesh_bvh_root;
-    std::vector<Bvh4Node> bvh4_nodes; // the same BLAS collapsed to 4-wide nodes (persistent traces)
-    std::vector<int> mesh_bvh4_root;
-    int bvh4_max_depth = 0;           // deepest BVH4 node level (root = 1), all meshes
 
     RenderSettings settings;          // optional RENDER block of the config
     std::string last_error;
@@ -108,7 +105,6 @@ private:
     void addMeshesToGrid();
     void buildDeviceTables();
     void buildBvh(int mesh);
-    void buildBvh4(int mesh);
     int relayoutPairs(int n0, int root);       // sibling inner nodes side by side (bvh.cpp)
     void world_box(const Model& m, const Mesh& mesh, int root, float* out) const;
 };

@@ -83,75 +83,3 @@ def test_depth_cap_on_degenerate_distribution(pt_mod):
     assert sum(c for _, c, _ in leaves) == n
 
 
-def _walk4(nodes, root):
-    """Leaves (first ref, count, slot box) of a 4-wide BLAS, and its depth."""
-    ints = nodes.view(np.int32)
-    leaves, depth_max = [], 0
-    stack = [(root, 1)]
-    while stack:
-        n, d = stack.pop()
-        depth_max = max(depth_max, d)
-        for c in range(4):
-            cnt = ints[n, 28 + c]
-            if cnt < 0:
-                continue
-            lo = nodes[n, [c, 8 + c, 16 + c]]
-            hi = nodes[n, [4 + c, 12 + c, 20 + c]]
-            if cnt == 0:
-                child = ints[n, 24 + c]
-                # the child's slots lie inside this slot's box
-                for cc in range(4):
-                    if ints[child, 28 + cc] >= 0:
-                        assert (nodes[child, [cc, 8 + cc, 16 + cc]] >= lo).all()
-                        assert (nodes[child, [4 + cc, 12 + cc, 20 + cc]] <= hi).all()
-                stack.append((child, d + 1))
-            else:
-                assert cnt <= 7
-                leaves.append((ints[n, 24 + c], cnt, (lo, hi)))
-    return leaves, depth_max
-
-
-@pytest.mark.parametrize("ntri", [10, 5000, 60000])
-def test_bvh4_collapse_covers_every_triangle(pt_mod, ntri):
-    from pathtracerap_amd.synthetic import torus_mesh
-    pos, nrm, tris = torus_mesh(ntri, seed=1)
-    s = pt_mod.Scene()
-    m = s.addMesh(pos, nrm, tris)
-    s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
-    s.build(bvh=True)
-    b, b4 = s.export_bvh(), s.export_bvh4()
-    a = s.export()
-    leaves, depth = _walk4(b4["nodes"], b4["roots"][0])
-    assert 3 * depth <= 24 + 64          # LDS stack + global spill entries per lane
-    seen = np.zeros(len(a["tris"]), np.int32)
-    V = a["vpos"].astype(np.float64)
-    for first, cnt, (lo, hi) in leaves:
-        for t in b["refs"][first:first + cnt]:
-            seen[t] += 1
-            p = V[a["tris"][t]]
-            e1, e2 = p[1] - p[0], p[2] - p[0]
-            for u, v in ((-0.005, -0.005), (1.01, -0.005), (-0.005, 1.01)):
-                q = p[0] + u * e1 + v * e2
-                assert (q >= lo - 1e-9).all() and (q <= hi + 1e-9).all()
-    assert (seen == 1).all()
-    if ntri >= 5000:
-        assert len(b4["nodes"]) < 0.6 * len(b["nodes"])     # really 4-wide
-
-
-def test_bvh4_oversized_leaves_are_chunked(pt_mod, monkeypatch):
-    """Leaves larger than a BVH4 slot holds (binary depth cap) become chunk nodes."""
-    from pathtracerap_amd.synthetic import torus_mesh
-    monkeypatch.setenv("PT_BVH_LEAF", "16")
-    import subprocess, sys, json, os
-    code = ("import json,sys; sys.path.insert(0, %r)\n" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))) +
-            "import numpy as np, pathtracerap_amd as P\n"
-            "from pathtracerap_amd.synthetic import torus_mesh\n"
-            "pos, nrm, tris = torus_mesh(3000, seed=2)\n"
-            "s = P.Scene(); m = s.addMesh(pos, nrm, tris)\n"
-            "s.addModel(m, (1,1,1), (0,0,0), (0,0,0), 'DIFFUSE', (1,1,1)); s.build(bvh=True)\n"
-            "b = s.export_bvh(); b4 = s.export_bvh4()\n"
-            "i2 = b['nodes'].view(np.int32); i4 = b4['nodes'].view(np.int32)\n"
-            "print(json.dumps([int(max(i2[:, 11].max(), i2[:, 15].max())), int(i4[:, 28:].max()), int(len(b['refs']))]))\n")
-    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=dict(os.environ), check=True)
-    max2, max4, nrefs = json.loads(out.stdout.strip().splitlines()[-1])
-    assert max2 > 7 and max4 <= 7 and nrefs > 2900

@@ -241,22 +241,21 @@ def test_grid_fast_hitset_overflow_falls_back_exactly(gpu, pt_mod, oracle_mod, a
 
 @pytest.mark.parametrize("accel,env", [
     (1, {"PT_TRACE_SPLIT": "0"}),
-    (1, {"PT_TRACE_FLAGS": "0"}),
-    (1, {"PT_TRACE_FLAGS": "3"}),
-    (1, {"PT_TRACE_FLAGS": "4", "PT_TRACE_REFILL": "1"}),
+    (1, {"PT_TRACE_FLAGS": "10"}),
+    (1, {"PT_TRACE_FLAGS": "10", "PT_TRACE_REFILL": "1"}),
     (1, {"PT_TRACE_FLAGS": "11", "PT_TRACE_WAVES_PER_CU": "1"}),
-    (1, {"PT_TRACE_FLAGS": "27"}),
-    (1, {"PT_TRACE_FLAGS": "19", "PT_BVH_LEAF": "16"}),
+    (1, {"PT_TRACE_FLAGS": "11", "PT_BVH_LEAF": "16"}),
     (2, {"PT_GF_SPLIT": "0"}),
-    (2, {"PT_GF_FLAGS": "0"}),
+    (2, {"PT_GF_FLAGS": "8"}),
     (2, {"PT_GF_FLAGS": "8", "PT_TRACE_REFILL": "1"}),
     (2, {"PT_TRACE_WAVES_PER_CU": "1"}),
-    (2, {"PT_GF_FLAGS": "13"}),
-    (2, {"PT_GF_FLAGS": "13", "PT_TRACE_REFILL": "1", "PT_TRACE_WAVES_PER_CU": "1"}),
+    (2, {"PT_TRACE_REFILL": "1", "PT_TRACE_WAVES_PER_CU": "1"}),
+    (2, {"PT_BVH_LEAF": "16"}),
 ])
 def test_trace_kernel_variants_bitexact(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, env):
-    """Every persistent-trace variant (fused / split, refill policy, phase
-    scheduling, one wave per CU) renders the oracle's image bit for bit."""
+    """Every persistent-trace variant (fused / split, model records in LDS or
+    global memory, refill policy, one wave per CU, oversized leaves) renders the
+    oracle's image bit for bit."""
     from pathtracerap_amd import synthetic
     P, O = pt_mod, oracle_mod
     for k, v in env.items():
@@ -510,44 +509,3 @@ def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypat
         assert deferred == 0, deferred
     else:
         assert deferred > 0
-
-
-@pytest.mark.parametrize("accel", [1, 2])
-@pytest.mark.parametrize("pipes", [1, 4])
-def test_hit_order_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, pipes):
-    """PT_HIT_ORDER=1: the persistent traces write hit records at the rays' claim
-    positions of the ray sort and the shading pass finds them through slot_pos;
-    deferred rays, drain continuations and walk hand-ons carry the position.
-    Images and segment counts stay the oracle's."""
-    from pathtracerap_amd import synthetic
-    P, O = pt_mod, oracle_mod
-    monkeypatch.setenv("PT_HIT_ORDER", "1")
-    for path in (synthetic.diffuse_scene(synth_dir, ntri=6000, seed=17, metallic=True), REF_SCENE):
-        s = P.Scene(path)
-        s.build()
-        cfg = P.RenderConfig(width=157, height=83, iterations=3, max_bounces=7, accel=accel, pipelines=pipes)
-        img, seg, oimg, oseg = _render_both(P, O, s, cfg)
-        assert seg == oseg
-        assert_bitexact(img, oimg, f"PT_HIT_ORDER accel={accel} pipes={pipes}")
-
-
-@pytest.mark.parametrize("accel", [1, 2])
-@pytest.mark.parametrize("pipes", [1, 4])
-@pytest.mark.parametrize("copy,hit_order", [("1", "0"), ("1", "1")])
-def test_sort_copy_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, pipes, copy, hit_order):
-    """PT_SORT_COPY=1: k_sort_scatter copies each ray, with its dense slot, to its
-    claim position, and the persistent traces' refills read it there (one
-    coalesced load instead of the claim-order entry and then the ray gather).
-    Only the claim path changes: images and segment counts stay the oracle's,
-    alone and with PT_HIT_ORDER."""
-    from pathtracerap_amd import synthetic
-    P, O = pt_mod, oracle_mod
-    monkeypatch.setenv("PT_SORT_COPY", copy)
-    monkeypatch.setenv("PT_HIT_ORDER", hit_order)
-    for path in (synthetic.diffuse_scene(synth_dir, ntri=6000, seed=23, metallic=True), REF_SCENE):
-        s = P.Scene(path)
-        s.build()
-        cfg = P.RenderConfig(width=149, height=91, iterations=3, max_bounces=7, accel=accel, pipelines=pipes)
-        img, seg, oimg, oseg = _render_both(P, O, s, cfg)
-        assert seg == oseg
-        assert_bitexact(img, oimg, f"PT_SORT_COPY={copy} PT_HIT_ORDER={hit_order} accel={accel} pipes={pipes}")
