@@ -1590,7 +1590,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
     unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_walk = 0, it_sel = 0;
-    unsigned long long cy[5] = {0, 0, 0, 0, 0};     // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node, walk
+    unsigned long long cy[6] = {0, 0, 0, 0, 0, 0};  // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node,
+                                                    // walk (certificates), hand-on / drain records
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
     unsigned long long ts = stamps ? clock64() : 0;
     for (unsigned iters = 0;; iters++) {
@@ -1924,7 +1925,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 state = 2;
             }
         }
+        if (stamps) { const unsigned long long t = clock64(); cy[4] += t - ts; ts = t; }
         if ((phase & 16) || (!TAIL && (phase & 8) && __ballot(state == 6))) {
+            if (PT_TRACE_STATS && (p.debug & 32) && lane == 0)     // walk iterations with hand-ons, drains
+                atomicAdd(p.segments + ((phase & 16) ? 27 : 26) + kMaxBounceCounters, 1ull);
             // hand-on records: the drain (phase 16: every busy lane's exact state, then
             // the wave is done) or walk hand-ons (state 6: a collected hit set the
             // certificate left undecided; the tail launch walks it exactly)
@@ -1969,10 +1973,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
             state = drain ? 3 : (state == 6 ? 0 : state);
         }
-        if (stamps) { const unsigned long long t = clock64(); cy[4] += t - ts; ts = t; }
+        if (stamps) { const unsigned long long t = clock64(); cy[5] += t - ts; ts = t; }
     }
     if (stamps && lane == 0)
-        for (int q = 0; q < 5; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
+        for (int q = 0; q < 6; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
         atomicAdd(p.segments + 44 + kMaxBounceCounters, st_drain);

@@ -92,9 +92,12 @@ def main():
             out[v]["busy_lanes_per_drain_iter"] = round(allc[108] / max(allc[107], 1), 2)
             out[v]["phase_iters_per_segment"] = {k: round(a / sg, 3) for k, (a, b) in ph.items()}
         if "PT_DEBUG_ABLATE=32" in v or "PT_DEBUG_ABLATE=96" in v:   # cycle stamps
-            cyc = allc[83:88]
+            cyc = allc[83:89]
             tot = max(sum(cyc), 1)
-            out[v]["cycle_share"] = dict(zip(["refill", "select", "leaf", "node", "walk"], [round(c / tot, 3) for c in cyc]))
+            out[v]["cycle_share"] = dict(zip(["refill", "select", "leaf", "node", "walk", "handon_drain"],
+                                             [round(c / tot, 3) for c in cyc]))
+            out[v]["handon_iters_per_segment"] = round(allc[89] / max(rs[v].segments(), 1), 5)
+            out[v]["drains_per_segment"] = round(allc[90] / max(rs[v].segments(), 1), 5)
             out[v]["wave_cycles_per_segment"] = round(tot / max(rs[v].segments(), 1), 1)
         if "PT_DEBUG_ABLATE=96" in v:
             w3 = allc[92:95]
