@@ -40,6 +40,10 @@ constexpr int kBlock = 256;
 #ifndef PT_HITCAP
 #define PT_HITCAP 6
 #endif
+#ifndef PT_CERT_MODE
+#define PT_CERT_MODE 1        // k_trace_gf main launch's walk decision: 0 walk_certify only, 1 walk_certify_fast
+                              // first, 2 walk_certify_fast only (the rest goes to the tail launch's exact walk)
+#endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
 #endif
@@ -753,6 +757,126 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
     if (!(t_box + te < tmin + win)) PT_CERT_FAIL(7)
 #undef PT_CERT_FAIL
     tri = bi;
+    return ok;
+}
+
+// Fast walk certificate: a cheaper sufficient condition for the common case,
+// tried before walk_certify.  It decides the walk's result as (t_min, m*) when
+// m* is the UNIQUE minimum-t member and the walk provably tests it before it
+// can stop.  The lemma both certificates rest on: at every walk parameter s
+// (from pt) the walk's voxel holds, per axis a, a point within
+// delta_a = cslack_a + |d_a| errm of the exact ray point ray(s) (the DDA's
+// +EPSILON start shift and its crossing-parameter rounding, errm bounding the
+// latter up to s).
+//  (i) B*, m*'s voxel box shrunk by delta, holds ray(s*) at s* = max(e, 0) + sl
+//      (e: B*'s exact entry, sl a rounding slack, s* + sl < B*'s exit): the
+//      walk's voxel at s* lies in m*'s box, so m* is tested no later than s* --
+//      unless the walk stopped before, which needs an earlier hit voxel.
+// (ii) A voxel of member h visited at s' puts ray(s') inside h's box grown by
+//      delta, so s' >= g_h, that grown box's entry.  Only h's voxels outside
+//      m*'s box matter (m*'s own voxels test m* too): when h's box leaves m*'s
+//      along one side of one axis only, that part is itself a box, else the
+//      whole box stands in for it.  g_h > s* (or a grown box the ray misses, or
+//      a start inside B*, whose start voxel then is m*'s) means no voxel before
+//      the walk reaches m*'s box is a hit voxel: the walk cannot stop before
+//      testing m*, and m*'s unique minimum t makes the result (t_min, m*).
+// (iii) The voxel holding s* was entered at a parameter <= s*: within the
+//      window when t_box + s* < t_min + win (plus rounding slack).
+// Any doubt (ties at t_min, zero slopes, boxes too thin to shrink, rays that
+// only graze B*) returns false and walk_certify / the exact walk decide.
+template <int CAP, class GetM>
+__device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
+                                                  GetM get, int nh, float tmin, float win, int& tri) {
+    int cnt = 0;
+    int4 ms = make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 e = get(h);
+        const bool mn = __int_as_float(e.x) == tmin;
+        cnt += mn ? 1 : 0;
+        ms = mn ? e : ms;
+    }
+    const float pp[3] = {pt.x, pt.y, pt.z}, dv[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z};
+    int bl[3], bh[3];
+    float lo[3], hi[3];
+    float sB = -3.0e38f, xB = 3.0e38f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        bl[a] = (ms.z >> (10 * a)) & 1023;
+        bh[a] = (ms.w >> (10 * a)) & 1023;
+        lo[a] = M.bbox[a] + (float)bl[a] * M.vw[a];
+        hi[a] = M.bbox[a] + (float)(bh[a] + 1) * M.vw[a];
+        const float s0 = (lo[a] - pp[a]) * iv[a], s1 = (hi[a] - pp[a]) * iv[a];
+        sB = fmaxf(sB, fminf(s0, s1));
+        xB = fminf(xB, fmaxf(s0, s1));
+    }
+    // crossing-parameter error bound for every parameter up to B*'s exit (walk_certify's formula)
+    float errm = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float span = M.vw[a] * (float)p.gdim[a];
+        errm = fmaxf(errm, 4.8e-7f * (float)(p.gdim[a] + 4) * (absr(xB) + 1.0f) +
+                               1e-6f * (absr(M.bbox[a]) + span + absr(pp[a])) * absr(iv[a]));
+    }
+    float dl[3];
+    float e = -3.0e38f, x = 3.0e38f;
+    bool thick = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        dl[a] = M.cslack[a] + absr(dv[a]) * errm;
+        const float L = lo[a] + dl[a], H = hi[a] - dl[a];
+        thick = thick & (L < H);
+        const float s0 = (L - pp[a]) * iv[a], s1 = (H - pp[a]) * iv[a];
+        e = fmaxf(e, fminf(s0, s1));
+        x = fminf(x, fmaxf(s0, s1));
+    }
+    const float sl = 1e-5f * (absr(x) + 1.0f);
+    const float ss = fmaxf(e, 0.0f) + sl;
+    bool ok = (cnt == 1) & (dv[0] != 0.0f) & (dv[1] != 0.0f) & (dv[2] != 0.0f) & thick & (sB <= xB) &
+              (ss + sl < x) & (absr(x) < 1e30f) & (errm < 1e30f);
+    const float tw = t_box + ss;
+    ok = ok & (tw + 1e-5f * (absr(tw) + 1.0f) < tmin + win);
+    const bool start_in = e < 0.0f;               // the walk's start voxel is m*'s
+#pragma unroll
+    for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
+        if (CAP > 0 && h >= nh) break;
+        const int4 m = get(h);
+        int ml[3], mh[3];
+        int ext = 0, ax = 0;
+        bool below = false;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            ml[a] = (m.z >> (10 * a)) & 1023;
+            mh[a] = (m.w >> (10 * a)) & 1023;
+            const bool lb = ml[a] < bl[a], ha = mh[a] > bh[a];
+            ext += (lb ? 1 : 0) + (ha ? 1 : 0);
+            ax = (lb | ha) ? a : ax;
+            below = (lb | ha) ? lb : below;
+        }
+        // one extension: only the part of h's box outside m*'s along axis ax can hold a
+        // voxel the walk visits before m*'s box
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const bool cut = (ext == 1) & (a == ax);
+            mh[a] = (cut & below) ? bl[a] - 1 : mh[a];
+            ml[a] = (cut & !below) ? bh[a] + 1 : ml[a];
+        }
+        float g = -3.0e38f, go = 3.0e38f;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const float L = M.bbox[a] + (float)ml[a] * M.vw[a] - dl[a];
+            const float H = M.bbox[a] + (float)(mh[a] + 1) * M.vw[a] + dl[a];
+            const float s0 = (L - pp[a]) * iv[a], s1 = (H - pp[a]) * iv[a];
+            g = fmaxf(g, fminf(s0, s1));
+            go = fminf(go, fmaxf(s0, s1));
+        }
+        const bool mn = __int_as_float(m.x) == tmin;
+        const bool missed = (g > go + 1e-5f * (absr(go) + 1.0f)) & (absr(g) < 1e30f);
+        const bool after = (g - 1e-5f * (absr(g) + 1.0f) > ss) & (absr(g) < 1e30f);
+        ok = ok & (mn | (ext == 0) | start_in | missed | after);
+    }
+    tri = ms.y;
     return ok;
 }
 
@@ -1897,11 +2021,21 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             } else if (!TAIL && !(F & 16)) {
                 // the certificate only; a ray it cannot decide is handed on to the tail launch
                 // (which walks it exactly) or, past the records' room, to k_trace_deferred
+                // (hit sets in a global pool block -- more than kGfHitCap members, rare -- are
+                // handed on undecided: the pool's runtime-length loops would cost registers here)
                 int tri = -1;
-                const int4* g = p.hs_pool + (size_t)max(pblk, 0) * kHitCapPool;
-                const bool ok = pblk < 0
-                    ? walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, [&](int h) { return hs[h * BS]; }, nh, tmin, win, tri)
-                    : walk_certify<0>(p, M, d, inv, pt, t_box, [&](int h) { return g[h]; }, nh, tmin, win, tri);
+                auto lds_get = [&](int h) { return hs[h * BS]; };
+                bool ok = false;
+                if (PT_CERT_MODE >= 1 && pblk < 0)
+                    ok = walk_certify_fast<kGfHitCap>(p, M, d, inv, pt, t_box, lds_get, nh, tmin, win, tri);
+                if (PT_TRACE_STATS && (p.debug & 4)) {
+                    atomicAdd(p.segments + 42 + kMaxBounceCounters, 1ull);
+                    if (ok) atomicAdd(p.segments + 40 + kMaxBounceCounters, 1ull);
+                }
+                if (PT_CERT_MODE <= 1 && !ok && pblk < 0) {
+                    ok = walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, lds_get, nh, tmin, win, tri);
+                    if (PT_TRACE_STATS && (p.debug & 4) && ok) atomicAdd(p.segments + 41 + kMaxBounceCounters, 1ull);
+                }
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
                 if (!ok) state = 6;
             } else {

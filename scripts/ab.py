@@ -112,6 +112,10 @@ def main():
         if allc[86]:
             out[v]["collect_nodes_per_collection"] = round(allc[85] / allc[86], 2)
             out[v]["collections_per_segment"] = round(allc[86] / rs[v].segments(), 3)
+        if allc[105]:                                  # slots 40..42: fast / full certificate outcomes
+            out[v]["cert_attempts_per_segment"] = round(allc[105] / max(rs[v].segments(), 1), 5)
+            out[v]["cert_fast_ok_share"] = round(allc[103] / allc[105], 4)
+            out[v]["cert_full_ok_after_fast_share"] = round(allc[104] / allc[105], 4)
         cf = allc[95:103]
         if any(cf):
             out[v]["cert_fail_per_segment"] = dict(zip(["ties", "zero_dir", "start_shift", "starts_in_U", "grazes_U",
