@@ -74,6 +74,8 @@ def parse(argv=None):
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--metallic", action="store_true")
+    ap.add_argument("--inmem", action="store_true", help="build the synthetic scene in memory (addMesh / addModel) "
+                                                        "instead of through OBJ text (10M triangles: minutes of text)")
     ap.add_argument("--scene", default="", help="a scene file instead of the synthetic OBJ scene (e.g. "
                                                 "scenes/reference_scene.txt); its RENDER block's bounces apply")
     ap.add_argument("--targets", default="target_1m,configs2,configs4",
@@ -165,19 +167,17 @@ def host_cpu_share():
     return max(1, n), ", ".join(why)
 
 
-def cpu_baseline(scene_path, bounces, width, height, target_s):
+def cpu_baseline(scene, bounces, width, height, target_s):
     """The oracle (C port of the reference's bounce loop) on the host cores:
-    same scene and camera, reduced resolution, 1 sample per pixel, sized to
-    about ``target_s`` seconds of CPU work."""
+    same scene (the built product Scene's export) and camera, reduced
+    resolution, 1 sample per pixel, sized to about ``target_s`` seconds of CPU
+    work."""
     import oracle as O
-    import pathtracerap_amd as P
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import flat_from_export
 
     threads, share = host_cpu_share()
-    s = P.Scene(scene_path)
-    s.build()
-    flat = flat_from_export(s.export())
+    flat = flat_from_export(scene.export())
 
     def run(w, h, iters):
         cfg = O.RenderConfig(width=w, height=h, iterations=iters, max_bounces=bounces, accel=0, threads=threads)
@@ -393,9 +393,12 @@ def main():
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.hw_queues > 0:     # read once by the HIP runtime at initialisation: set before torch touches it
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
-    import pathtracerap_amd as P            # loads the library before HIP starts (its load-time checks)
+    # torch first: its HIP runtime is the process's (libpathtracer_amd.so then binds to it; loaded
+    # before torch, the library's own /opt/rocm runtime left torch's allocations without a device)
     import torch
     import torch.distributed as dist
+
+    import pathtracerap_amd as P
 
     # one rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on a 1-GPU
     # box) ranks share devices round-robin
@@ -414,21 +417,26 @@ def main():
 
     accels = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}
     tmp = tempfile.mkdtemp(prefix=f"ptbench_r{rank}_")
-    if args.scene:
-        scene_path = os.path.abspath(args.scene)
-    else:
-        scene_path = synthetic.diffuse_scene(tmp, ntri=args.ntri, width=args.width, height=args.height,
-                                             bounces=args.bounces, accel=args.accel, metallic=args.metallic)
     accel = accels[args.accel]
-    scene = P.Scene(scene_path)
-    cfg = scene.apply_settings(P.RenderConfig())
+    if args.inmem and not args.scene:
+        scene = synthetic.build_scene(P, args.ntri, metallic=args.metallic, bvh=accel != P.ACCEL_GRID)
+        cfg = P.RenderConfig()
+    else:
+        if args.scene:
+            scene_path = os.path.abspath(args.scene)
+        else:
+            scene_path = synthetic.diffuse_scene(tmp, ntri=args.ntri, width=args.width, height=args.height,
+                                                 bounces=args.bounces, accel=args.accel, metallic=args.metallic)
+        scene = P.Scene(scene_path)
+        cfg = scene.apply_settings(P.RenderConfig())
     cfg.width, cfg.height, cfg.accel = args.width, args.height, accel
     if not args.scene:
         cfg.max_bounces = args.bounces
     args.bounces = cfg.max_bounces
     if args.pipelines > 0:
         cfg.pipelines = args.pipelines
-    scene.build(grid=cfg.grid, bvh=accel != P.ACCEL_GRID)
+    if not (args.inmem and not args.scene):
+        scene.build(grid=cfg.grid, bvh=accel != P.ACCEL_GRID)
     ntri = scene.counts()["nt"]
     npix = cfg.width * cfg.height
     K, W = args.steps, args.warmup
@@ -558,7 +566,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(scene_path, args.bounces, cfg.width, cfg.height, args.cpu_seconds)
+                cpu = cpu_baseline(scene, args.bounces, cfg.width, cfg.height, args.cpu_seconds)
             except Exception as e:  # noqa: BLE001 -- reported, not fatal
                 cpu = {"error": repr(e)}
         out = {

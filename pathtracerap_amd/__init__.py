@@ -403,11 +403,3 @@ def render(scene_config: str, cfg: RenderConfig | None = None, bmp_out: str | No
     (pt_default_config) overlaid with the scene file's RENDER block."""
     c = ctypes.byref(cfg.c()) if cfg is not None else None
     _err(lib().pt_render(os.fsencode(scene_config), c, os.fsencode(bmp_out) if bmp_out else None), "render")
-
-
-# Load the library when the package is imported: its load-time default
-# (GPU_MAX_HW_QUEUES=16, one hardware queue per pipeline stream) only takes
-# effect if it runs before the process starts HIP.  A missing library is not an
-# error here (build() may follow); every call into it raises.
-if os.path.exists(_LIB_PATH):
-    lib()

@@ -44,6 +44,9 @@ constexpr int kBlock = 256;
 #define PT_CERT_MODE 1        // k_trace_gf main launch's walk decision: 0 walk_certify only, 1 walk_certify_fast
                               // first, 2 walk_certify_fast only (the rest goes to the tail launch's exact walk)
 #endif
+#ifndef PT_GF_VBOX
+#define PT_GF_VBOX 1          // k_trace_gf node pruning on the children's voxel-box unions (else: node box + a voxel)
+#endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
 #endif
@@ -1968,8 +1971,25 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             // non-short-circuit: both children's slabs in one basic block (a branch on
             // cnt >= 0 moved the float work into its own block, where every min/max
             // operand was re-canonicalised)
+#if PT_GF_VBOX
+            // A child is needed if it can hold a hit nearer than t_min (its box entered by
+            // then: t_min stays the true minimum) or a required member (its triangles'
+            // voxel-box union, grown by cslack, entered before the window's end; the entry
+            // computed as vbox_entry computes a member's, so it is <= every member's).
+            const float4 v0 = p.bvh_vbox[3 * cur], v1 = p.bvh_vbox[3 * cur + 1], v2 = p.bvh_vbox[3 * cur + 2];
+            const float tv0 = fmaxf(fmaxf(fminf((v0.x - o.x) * ninv.x, (v0.w - o.x) * ninv.x),
+                                          fminf((v0.y - o.y) * ninv.y, (v1.x - o.y) * ninv.y)),
+                                    fminf((v0.z - o.z) * ninv.z, (v1.y - o.z) * ninv.z));
+            const float tv1 = fmaxf(fmaxf(fminf((v1.z - o.x) * ninv.x, (v2.y - o.x) * ninv.x),
+                                          fminf((v1.w - o.y) * ninv.y, (v2.z - o.y) * ninv.y)),
+                                    fminf((v2.x - o.z) * ninv.z, (v2.w - o.z) * ninv.z));
+            const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & ((tn0 <= tmin) | (tv0 <= bound));
+            const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & ((tn1 <= tmin) | (tv1 <= bound));
+            (void)tx0; (void)tx1;
+#else
             const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
             const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
+#endif
             // the step's decisions as selects; only the push and the pop touch memory
             // (the traces are issue-bound: every divergent branch costs scalar exec-mask work)
             const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
@@ -2582,6 +2602,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
+    PT_HIP(upload(allocs, &kp.bvh_vbox, scene.bvh_vbox.data(), scene.bvh_vbox.size() * sizeof(float), stream));
 
     kp.width = cfg.width;
     kp.height = cfg.height;

@@ -11,6 +11,7 @@
 #   ktrace[=ARGS]         rocprofv3 --kernel-trace of bench.py ARGS + scripts/timeline.py
 #   pmc[=ARGS]            FETCH_SIZE and WRITE_SIZE, one --pmc pass each, of bench.py ARGS
 #   counters=C1,C2@ARGS   one --pmc pass of the listed counters (within one pass's limits)
+#   vcounters=LIB@C1,C2@ARGS  the same against build_variants/lib_LIB.so ("default" = in-tree)
 #   ab=ARGS               python scripts/ab.py ARGS (interleaved in-process A/B)
 #   ablib=R@SPEC@N1,N2    R interleaved rounds of ab.py SPEC over library builds
 #                         (build_variants/lib_N.so from scripts/build_variant.sh; "default" = in-tree)
@@ -64,6 +65,12 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc ${c//,/ } -d gpurun_out/$tag -o run --output-format csv -- python3 bench.py $a > gpurun_out/$tag.log 2>&1
       rc=$?; tail -2 gpurun_out/$tag.log
       [ $rc -eq 0 ] && { python3 scripts/pmc_table.py gpurun_out/$tag; rc=$?; } ;;
+    vcounters)
+      IFS=@ read -r lib c a <<< "$arg"
+      if [ "$lib" = default ]; then L=$PWD/pathtracerap_amd/libpathtracer_amd.so; else L=$PWD/build_variants/lib_$lib.so; fi
+      PT_LIB_PATH=$L timeout -s KILL 300 rocprofv3 --pmc ${c//,/ } -d gpurun_out/$tag -o run --output-format csv -- python3 bench.py $a > gpurun_out/$tag.log 2>&1
+      rc=$?; tail -2 gpurun_out/$tag.log
+      [ $rc -eq 0 ] && { python3 scripts/pmc_table.py gpurun_out/$tag > gpurun_out/$tag.txt; rc=$?; grep -A6 "k_trace_gf" gpurun_out/$tag.txt | head -20; } ;;
     ab)
       timeout -k 10 900 python -u scripts/ab.py $arg > gpurun_out/$tag.json 2> gpurun_out/$tag.err
       rc=$?; cat gpurun_out/$tag.json; tail -3 gpurun_out/$tag.err ;;

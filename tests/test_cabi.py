@@ -57,11 +57,11 @@ def test_library_load_sets_hw_queues_unless_chosen():
 
 def test_hw_queue_info_reports_the_setting_found_at_load():
     """pt_hw_queue_info / hw_queues(): the value the process had chosen (or that
-    the library set 16); importing the package loads the library."""
+    the library set 16)."""
     import subprocess
     import sys
-    code = ("import sys; sys.path.insert(0, %r); import pathtracerap_amd as P; print(P._lib is not None, "
-            "P.hw_queues())") % ROOT
+    code = ("import sys; sys.path.insert(0, %r); import pathtracerap_amd as P; q = P.hw_queues(); "
+            "print(P._lib is not None, q)") % ROOT
     env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
     assert out.startswith("True ") and "'at_library_load': None, 'set_by_library': True, 'env_now': 16" in out, out
