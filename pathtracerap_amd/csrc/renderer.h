@@ -45,7 +45,6 @@ struct KParams {
     const int2* voxels;         // (start, end)
     const int* per_voxel;
     const BvhNode* bvh;
-    const float4* bvh_vbox;     // 3 float4 per BLAS node: per child its triangles' voxel-box union (k_trace_gf)
     const int* bvh_tri;
     const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
     int* spill;                 // traversal-stack spill beyond the LDS entries, lane-minor

@@ -44,8 +44,8 @@ constexpr int kBlock = 256;
 #define PT_CERT_MODE 1        // k_trace_gf main launch's walk decision: 0 walk_certify only, 1 walk_certify_fast
                               // first, 2 walk_certify_fast only (the rest goes to the tail launch's exact walk)
 #endif
-#ifndef PT_GF_VBOX
-#define PT_GF_VBOX 1          // k_trace_gf node pruning on the children's voxel-box unions (else: node box + a voxel)
+#ifndef PT_PRECLAIM
+#define PT_PRECLAIM 1         // k_trace_gf main launch: claim the next refill's rays one refill ahead
 #endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
@@ -791,14 +791,16 @@ template <int CAP, class GetM>
 __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                                   GetM get, int nh, float tmin, float win, int& tri) {
     int cnt = 0;
-    int4 ms = make_int4(0, 0, 0, 0);
-#pragma unroll
+    int ms_y = 0, ms_z = 0, ms_w = 0;              // m*'s index and packed voxel box (per component:
+#pragma unroll                                     // a select of whole int4s went through scratch memory)
     for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
         if (CAP > 0 && h >= nh) break;
         const int4 e = get(h);
         const bool mn = __int_as_float(e.x) == tmin;
         cnt += mn ? 1 : 0;
-        ms = mn ? e : ms;
+        ms_y = mn ? e.y : ms_y;
+        ms_z = mn ? e.z : ms_z;
+        ms_w = mn ? e.w : ms_w;
     }
     const float pp[3] = {pt.x, pt.y, pt.z}, dv[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z};
     int bl[3], bh[3];
@@ -806,8 +808,8 @@ __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelR
     float sB = -3.0e38f, xB = 3.0e38f;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        bl[a] = (ms.z >> (10 * a)) & 1023;
-        bh[a] = (ms.w >> (10 * a)) & 1023;
+        bl[a] = (ms_z >> (10 * a)) & 1023;
+        bh[a] = (ms_w >> (10 * a)) & 1023;
         lo[a] = M.bbox[a] + (float)bl[a] * M.vw[a];
         hi[a] = M.bbox[a] + (float)(bh[a] + 1) * M.vw[a];
         const float s0 = (lo[a] - pp[a]) * iv[a], s1 = (hi[a] - pp[a]) * iv[a];
@@ -879,7 +881,7 @@ __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelR
         const bool after = (g - 1e-5f * (absr(g) + 1.0f) > ss) & (absr(g) < 1e30f);
         ok = ok & (mn | (ext == 0) | start_in | missed | after);
     }
-    tri = ms.y;
+    tri = ms_y;
     return ok;
 }
 
@@ -1712,6 +1714,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     float t_box = 0.0f, tmin = kFMax, win = 0.0f;
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
+    int pre = 0, pre_ok = 0;                        // PT_PRECLAIM: lane 0's claim for the next refill; pending?
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
     bool exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
@@ -1774,13 +1777,35 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
         } else if (!TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
-            const int leader = __ffsll((long long)idle) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(p.trace_next, cnt);
-            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
-            if (base + cnt >= n) exhausted = true;
+            const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+            int j0;
+            if (PT_PRECLAIM && pre_ok) {
+                // Q positions claimed at the previous refill (their atomic returned long ago; at
+                // least Q lanes are idle at every refill); more idle lanes claim the rest now
+                const int Q = p.trace_refill;
+                const int base = __builtin_amdgcn_readlane(pre, 0);
+                int b2 = 0;
+                if (cnt > Q && lane == 0) b2 = atomicAdd(p.trace_next, cnt - Q);
+                b2 = __builtin_amdgcn_readlane(b2, 0);
+                if (base + Q >= n || (cnt > Q && b2 + (cnt - Q) >= n)) exhausted = true;
+                j0 = rank < Q ? base + rank : b2 + (rank - Q);
+            } else {
+                const int leader = __ffsll((long long)idle) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(p.trace_next, cnt);
+                base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
+                if (base + cnt >= n) exhausted = true;
+                j0 = base + rank;
+            }
+            // claim the next refill's Q positions now: the atomic's round trip overlaps the
+            // traversal steps until then (its result is read at the next refill only)
+            pre_ok = 0;
+            if (PT_PRECLAIM && !exhausted) {
+                if (lane == 0) pre = atomicAdd(p.trace_next, p.trace_refill);
+                pre_ok = 1;
+            }
             if (state == 0) {
-                j = base + __popcll(idle & ((1ull << lane) - 1ull));
+                j = j0;
                 if (j < n) {
                     int src;
                     if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
@@ -1971,25 +1996,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             // non-short-circuit: both children's slabs in one basic block (a branch on
             // cnt >= 0 moved the float work into its own block, where every min/max
             // operand was re-canonicalised)
-#if PT_GF_VBOX
-            // A child is needed if it can hold a hit nearer than t_min (its box entered by
-            // then: t_min stays the true minimum) or a required member (its triangles'
-            // voxel-box union, grown by cslack, entered before the window's end; the entry
-            // computed as vbox_entry computes a member's, so it is <= every member's).
-            const float4 v0 = p.bvh_vbox[3 * cur], v1 = p.bvh_vbox[3 * cur + 1], v2 = p.bvh_vbox[3 * cur + 2];
-            const float tv0 = fmaxf(fmaxf(fminf((v0.x - o.x) * ninv.x, (v0.w - o.x) * ninv.x),
-                                          fminf((v0.y - o.y) * ninv.y, (v1.x - o.y) * ninv.y)),
-                                    fminf((v0.z - o.z) * ninv.z, (v1.y - o.z) * ninv.z));
-            const float tv1 = fmaxf(fmaxf(fminf((v1.z - o.x) * ninv.x, (v2.y - o.x) * ninv.x),
-                                          fminf((v1.w - o.y) * ninv.y, (v2.z - o.y) * ninv.y)),
-                                    fminf((v2.x - o.z) * ninv.z, (v2.w - o.z) * ninv.z));
-            const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & ((tn0 <= tmin) | (tv0 <= bound));
-            const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & ((tn1 <= tmin) | (tv1 <= bound));
-            (void)tx0; (void)tx1;
-#else
             const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
             const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
-#endif
             // the step's decisions as selects; only the push and the pop touch memory
             // (the traces are issue-bound: every divergent branch costs scalar exec-mask work)
             const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
@@ -2033,7 +2041,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 atomicAdd(p.segments + 51 + (pblk >= 0 ? 3 : min(nh, 4) - 1) + kMaxBounceCounters, 1ull);
             const ModelRec& M = models[im];
             const f3 pt = o + d * t_box;
-            const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
             WalkResult w;
             if (PT_TRACE_STATS && (p.debug & 128) && pblk < 0) {      // timing-only ablation: no walk at all
                 w.hit = true; w.has_best = true; w.final_min = true; w.t = tmin; w.tri = -1; w.tw = 0.0f;
@@ -2043,22 +2050,32 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 // (which walks it exactly) or, past the records' room, to k_trace_deferred
                 // (hit sets in a global pool block -- more than kGfHitCap members, rare -- are
                 // handed on undecided: the pool's runtime-length loops would cost registers here)
+                // members copied to registers first: four LDS reads issued together, one wait
+                // (read member by member inside the certificates' loops, every read waited
+                // on its own)
                 int tri = -1;
-                auto lds_get = [&](int h) { return hs[h * BS]; };
+                int4 mem[kGfHitCap];
+#pragma unroll
+                for (int h = 0; h < kGfHitCap; h++) mem[h] = hs[h * BS];
+                auto lds_get = [&](int h) { return mem[h]; };
                 bool ok = false;
-                if (PT_CERT_MODE >= 1 && pblk < 0)
-                    ok = walk_certify_fast<kGfHitCap>(p, M, d, inv, pt, t_box, lds_get, nh, tmin, win, tri);
+                // ninv (1/d clamped to +-1e30, set at select) is the exact 1/d when no slope is clamped
+                const bool exact_inv = (absr(ninv.x) < 1e30f) & (absr(ninv.y) < 1e30f) & (absr(ninv.z) < 1e30f);
+                if (PT_CERT_MODE >= 1 && pblk < 0 && exact_inv)
+                    ok = walk_certify_fast<kGfHitCap>(p, M, d, ninv, pt, t_box, lds_get, nh, tmin, win, tri);
                 if (PT_TRACE_STATS && (p.debug & 4)) {
                     atomicAdd(p.segments + 42 + kMaxBounceCounters, 1ull);
                     if (ok) atomicAdd(p.segments + 40 + kMaxBounceCounters, 1ull);
                 }
                 if (PT_CERT_MODE <= 1 && !ok && pblk < 0) {
+                    const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                     ok = walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, lds_get, nh, tmin, win, tri);
                     if (PT_TRACE_STATS && (p.debug & 4) && ok) atomicAdd(p.segments + 41 + kMaxBounceCounters, 1ull);
                 }
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
                 if (!ok) state = 6;
             } else {
+                const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
                              : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
                                                     tmin, win);
@@ -2602,7 +2619,6 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
-    PT_HIP(upload(allocs, &kp.bvh_vbox, scene.bvh_vbox.data(), scene.bvh_vbox.size() * sizeof(float), stream));
 
     kp.width = cfg.width;
     kp.height = cfg.height;

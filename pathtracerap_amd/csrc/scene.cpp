@@ -647,69 +647,6 @@ void Scene::buildDeviceTables() {
     }
 }
 
-// Voxel-box planes of every BLAS child for k_trace_gf's node pruning.  A member
-// h of a collection matters only if the walk can enter its voxel box before the
-// window's end: vbox_entry's test on the planes l = (B0 + lo * vw) - cslack and
-// h = (B0 + (hi + 1) * vw) + cslack (float, this exact expression order).  A
-// child's planes are the minimum / maximum of those floats over its subtree's
-// triangles, so the exact-ray entry of the child's box computed the same way
-// ((l - o) * inv per axis, monotone in l and h) is <= every member's: a child
-// entered after the window holds no required member.
-void Scene::buildBvhVoxelBoxes() {
-    bvh_vbox.assign(bvh_nodes.size() * 12, 0.0f);
-    for (size_t m = 0; m < meshes.size(); m++) {
-        const int root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m];
-        if (root < 0) continue;
-        int gi = -1;
-        for (const Model& md : models)
-            if (md.mesh_index == (int)m) { gi = md.grid_index; break; }
-        if (gi < 0) continue;
-        const Grid& g = grids[gi];
-        const BoundingBox& bb = meshes[m].bounding_box;
-        const float b0[3] = {bb.min.x, bb.min.y, bb.min.z};
-        float cs[3];
-        for (int k = 0; k < 3; k++) {     // ModelRec::cslack (buildDeviceTables), a property of the mesh's grid
-            const double span = (double)g.voxel_width[k] * grid_dim[k];
-            const double mag = std::fabs((double)(&bb.min.x)[k]) + std::fabs((double)(&bb.max.x)[k]) + span;
-            cs[k] = (float)(2.0 * kEps + 4.8e-7 * (grid_dim[k] + 4) * mag);
-        }
-        // post-order over the binary BLAS; box[6] = lo.xyz hi.xyz
-        struct Fn {
-            Scene* S; const float* b0; const float* vw; const float* cs;
-            void leaf(int first, int count, float* box) const {
-                for (int i = first; i < first + count; i++) {
-                    const int t = S->bvh_tri_order[i];
-                    const int lo = S->tri_vbox[2 * (size_t)t], hi = S->tri_vbox[2 * (size_t)t + 1];
-                    for (int a = 0; a < 3; a++) {
-                        const float l = (b0[a] + (float)((lo >> (10 * a)) & 1023) * vw[a]) - cs[a];
-                        const float h = (b0[a] + (float)(((hi >> (10 * a)) & 1023) + 1) * vw[a]) + cs[a];
-                        box[a] = std::min(box[a], l);
-                        box[3 + a] = std::max(box[3 + a], h);
-                    }
-                }
-            }
-            void node(int n, float* out) const {      // out: union of both children
-                const BvhNode nd = S->bvh_nodes[n];
-                const int cnt[2] = {nd.count0, nd.count1}, link[2] = {nd.link0, nd.link1};
-                float* rec = &S->bvh_vbox[(size_t)n * 12];
-                for (int c = 0; c < 2; c++) {
-                    float box[6] = {3e38f, 3e38f, 3e38f, -3e38f, -3e38f, -3e38f};
-                    if (cnt[c] > 0) leaf(link[c], cnt[c], box);
-                    else if (cnt[c] == 0) node(link[c], box);
-                    for (int k = 0; k < 6; k++) rec[6 * c + k] = box[k];
-                    for (int a = 0; a < 3; a++) {
-                        out[a] = std::min(out[a], box[a]);
-                        out[3 + a] = std::max(out[3 + a], box[3 + a]);
-                    }
-                }
-            }
-        };
-        const Fn f{this, b0, g.voxel_width, cs};
-        float all[6] = {3e38f, 3e38f, 3e38f, -3e38f, -3e38f, -3e38f};
-        f.node(root, all);
-    }
-}
-
 // Conservative world AABB of an instance (instance culling in the kernels):
 // the mesh bbox united with every triangle grown by the reference test's
 // barycentric tolerances (all points the test can accept), grown by 1e-3 of
@@ -776,7 +713,6 @@ int Scene::build(const int gd[3], bool with_bvh) {
     if (with_bvh)
         for (size_t m = 0; m < meshes.size(); m++) buildBvh((int)m);
     buildDeviceTables();
-    if (with_bvh) buildBvhVoxelBoxes();
     built = true;
     return 0;
 }

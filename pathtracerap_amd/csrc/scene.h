@@ -95,8 +95,6 @@ public:
                                       // the triangle index and its packed grid voxel box (mn, mx; 10 bits/axis)
     std::vector<int> tri_vbox;        // 2 ints / triangle: packed computeVoxelIndex min / max
     std::vector<int> mesh_bvh_root;
-    std::vector<float> bvh_vbox;      // 12 floats / BLAS node: per child the union of its triangles' voxel
-                                      // boxes as grown walk planes (c0 lo.xyz hi.xyz, c1 lo.xyz hi.xyz)
 
     RenderSettings settings;          // optional RENDER block of the config
     std::string last_error;
@@ -107,7 +105,6 @@ private:
     void addMeshesToGrid();
     void buildDeviceTables();
     void buildBvh(int mesh);
-    void buildBvhVoxelBoxes();
     int relayoutPairs(int n0, int root);       // sibling inner nodes side by side (bvh.cpp)
     void world_box(const Model& m, const Mesh& mesh, int root, float* out) const;
 };
