@@ -44,9 +44,6 @@ constexpr int kBlock = 256;
 #define PT_CERT_MODE 1        // k_trace_gf main launch's walk decision: 0 walk_certify only, 1 walk_certify_fast
                               // first, 2 walk_certify_fast only (the rest goes to the tail launch's exact walk)
 #endif
-#ifndef PT_PRECLAIM
-#define PT_PRECLAIM 1         // k_trace_gf main launch: claim the next refill's rays one refill ahead
-#endif
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0      // 1: diagnostic counters / timing ablations (PT_DEBUG_ABLATE); cost registers
 #endif
@@ -1714,7 +1711,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     float t_box = 0.0f, tmin = kFMax, win = 0.0f;
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
-    int pre = 0, pre_ok = 0;                        // PT_PRECLAIM: lane 0's claim for the next refill; pending?
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
     bool exhausted = false;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
@@ -1777,35 +1773,13 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
         } else if (!TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
             const int cnt = __popcll(idle);
-            const int rank = __popcll(idle & ((1ull << lane) - 1ull));
-            int j0;
-            if (PT_PRECLAIM && pre_ok) {
-                // Q positions claimed at the previous refill (their atomic returned long ago; at
-                // least Q lanes are idle at every refill); more idle lanes claim the rest now
-                const int Q = p.trace_refill;
-                const int base = __builtin_amdgcn_readlane(pre, 0);
-                int b2 = 0;
-                if (cnt > Q && lane == 0) b2 = atomicAdd(p.trace_next, cnt - Q);
-                b2 = __builtin_amdgcn_readlane(b2, 0);
-                if (base + Q >= n || (cnt > Q && b2 + (cnt - Q) >= n)) exhausted = true;
-                j0 = rank < Q ? base + rank : b2 + (rank - Q);
-            } else {
-                const int leader = __ffsll((long long)idle) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(p.trace_next, cnt);
-                base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
-                if (base + cnt >= n) exhausted = true;
-                j0 = base + rank;
-            }
-            // claim the next refill's Q positions now: the atomic's round trip overlaps the
-            // traversal steps until then (its result is read at the next refill only)
-            pre_ok = 0;
-            if (PT_PRECLAIM && !exhausted) {
-                if (lane == 0) pre = atomicAdd(p.trace_next, p.trace_refill);
-                pre_ok = 1;
-            }
+            const int leader = __ffsll((long long)idle) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(p.trace_next, cnt);
+            base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
+            if (base + cnt >= n) exhausted = true;
             if (state == 0) {
-                j = j0;
+                j = base + __popcll(idle & ((1ull << lane) - 1ull));
                 if (j < n) {
                     int src;
                     if (p.order) { const int2 e = p.order[j]; j = e.x; src = e.y; }   // sorted claim order
