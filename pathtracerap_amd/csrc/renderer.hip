@@ -1719,6 +1719,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     unsigned long long cy[6] = {0, 0, 0, 0, 0, 0};  // PT_DEBUG_ABLATE & 32: cycles in refill, select, leaf, node,
                                                     // walk (certificates), hand-on / drain records
     const bool stamps = PT_TRACE_STATS && (p.debug & 32);
+    unsigned long long cyr[4] = {0, 0, 0, 0};      // refill: claim, -, order entry + ray gather, stores drained before
     unsigned long long ts = stamps ? clock64() : 0;
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
@@ -1772,11 +1773,24 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 }
             }
         } else if (!TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+            // refill sub-stamps (stats build, PT_DEBUG_ABLATE & 32): every wait forced where it is
+            // stamped, so the claim, the claim-order entry and the ray gather are timed apart
+            auto rstamp = [&](int q) {
+                if (stamps) {
+                    __builtin_amdgcn_s_waitcnt(0);
+                    const unsigned long long t = clock64();
+                    cyr[q] += t - ts;
+                    cy[0] += t - ts;
+                    ts = t;
+                }
+            };
+            rstamp(3);
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.trace_next, cnt);
             base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
+            rstamp(0);
             if (base + cnt >= n) exhausted = true;
             if (state == 0) {
                 j = base + __popcll(idle & ((1ull << lane) - 1ull));
@@ -1794,6 +1808,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     state = 3;
                 }
             }
+            rstamp(2);
         }
         if (exhausted && state == 0) state = 3;
         if (__ballot(state != 3) == 0) break;
@@ -2120,8 +2135,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         }
         if (stamps) { const unsigned long long t = clock64(); cy[5] += t - ts; ts = t; }
     }
-    if (stamps && lane == 0)
+    if (stamps && lane == 0) {
         for (int q = 0; q < 6; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
+        for (int q = 0; q < 4; q++) atomicAdd(p.segments + 55 + q + kMaxBounceCounters, cyr[q]);
+    }
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
         atomicAdd(p.segments + 44 + kMaxBounceCounters, st_drain);

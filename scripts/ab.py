@@ -96,6 +96,9 @@ def main():
             tot = max(sum(cyc), 1)
             out[v]["cycle_share"] = dict(zip(["refill", "select", "leaf", "node", "walk", "handon_drain"],
                                              [round(c / tot, 3) for c in cyc]))
+            rr = allc[118:122]                       # slots 55..58: refill claim / order+gather / -, pre-refill
+            out[v]["refill_split_share"] = dict(zip(["claim", "-", "order_and_gather", "stores_before"],
+                                                    [round(c / tot, 3) for c in rr]))
             out[v]["handon_iters_per_segment"] = round(allc[89] / max(rs[v].segments(), 1), 5)
             out[v]["drains_per_segment"] = round(allc[90] / max(rs[v].segments(), 1), 5)
             out[v]["wave_cycles_per_segment"] = round(tot / max(rs[v].segments(), 1), 1)
