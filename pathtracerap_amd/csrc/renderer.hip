@@ -2083,8 +2083,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                              : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
                                                     tmin, win);
             }
-            if (state == 6) {
-                // handed on below
+            if (state == 6 || state == 7) {
+                // handed on below (6), or waiting for the batched full certificate (7)
             } else if (tier == 2 || w.final_min || w.tw < tmin + win) {
                 if (w.hit && w.has_best) {
                     const float dd = model_hit_dist(M, o, d, w.t, ow);
