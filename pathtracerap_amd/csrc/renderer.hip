@@ -1820,7 +1820,18 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
         // the cap's kernel-argument load stays out of the loop's common path
         if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
-            if (lane == 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
+            // the faulting wave's lane states (slots 33..38: states 7, 0, 3, 1, 2/4/5, exhausted waves)
+            const int f7 = __popcll(__ballot(state == 7)), f0 = __popcll(__ballot(state == 0)),
+                      f3 = __popcll(__ballot(state == 3)), f1 = __popcll(__ballot(state == 1));
+            if (lane == 0) {
+                atomicAdd(p.segments + kTraceFaultCounter, 1ull);
+                atomicAdd(p.segments + 33 + kMaxBounceCounters, (unsigned long long)f7);
+                atomicAdd(p.segments + 34 + kMaxBounceCounters, (unsigned long long)f0);
+                atomicAdd(p.segments + 35 + kMaxBounceCounters, (unsigned long long)f3);
+                atomicAdd(p.segments + 36 + kMaxBounceCounters, (unsigned long long)f1);
+                atomicAdd(p.segments + 37 + kMaxBounceCounters, (unsigned long long)(64 - f7 - f0 - f3 - f1));
+                atomicAdd(p.segments + 38 + kMaxBounceCounters, exhausted ? 1ull : 0ull);
+            }
             break;
         }
         // Phase scheduling: one step kind per iteration -- the one most lanes are
@@ -2075,8 +2086,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 }
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
                 // a fast-certificate failure waits for the batched full certificate (state 7);
-                // a full-certificate failure, or a pool hit set, is handed on (state 6)
-                if (!ok) state = (kFullLater && !(phase & 32) && pblk < 0) ? 7 : 6;
+                // a full-certificate failure, or a pool hit set, is handed on (state 6); a
+                // certified ray (5, also out of state 7) takes the result handling below
+                state = ok ? 5 : (kFullLater && !(phase & 32) && pblk < 0) ? 7 : 6;
             } else {
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
