@@ -1666,13 +1666,8 @@ __device__ __forceinline__ void node_slab_g(const float* lo, const float* hi, f3
     tnx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
 }
 
-#ifndef PT_FULL_BATCH
-#define PT_FULL_BATCH 4       // k_trace_gf main launch: fast-certificate failures certified fully in batches of this
-#endif                        // many (0: at once, in the same walk step)
 template <int BS, int F, bool TAIL = false>
 __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) void k_trace_gf(KParams p, int bounce, int level) {
-    constexpr bool kFullLater = PT_FULL_BATCH > 0 && PT_CERT_MODE == 1 && !TAIL && !(F & 16);
-    constexpr int kFullBatch = PT_FULL_BATCH > 0 ? PT_FULL_BATCH : 1;
     static_assert(kCX + 9 + kGfStack + 4 * kGfHitCap <= kContFields, "continuation record too small");
     __shared__ int s_stack[kGfStack * BS];
     __shared__ int4 s_hs[kGfHitCap * BS];
@@ -1820,16 +1815,15 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
         // the cap's kernel-argument load stays out of the loop's common path
         if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
-            // the faulting wave's lane states (slots 33..38: states 7, 0, 3, 1, 2/4/5, exhausted waves)
-            const int f7 = __popcll(__ballot(state == 7)), f0 = __popcll(__ballot(state == 0)),
-                      f3 = __popcll(__ballot(state == 3)), f1 = __popcll(__ballot(state == 1));
+            // the faulting wave's lanes (slots 34..38: idle, done, select, node/leaf/walk; exhausted waves)
+            const int f0 = __popcll(__ballot(state == 0)), f3 = __popcll(__ballot(state == 3)),
+                      f1 = __popcll(__ballot(state == 1));
             if (lane == 0) {
                 atomicAdd(p.segments + kTraceFaultCounter, 1ull);
-                atomicAdd(p.segments + 33 + kMaxBounceCounters, (unsigned long long)f7);
                 atomicAdd(p.segments + 34 + kMaxBounceCounters, (unsigned long long)f0);
                 atomicAdd(p.segments + 35 + kMaxBounceCounters, (unsigned long long)f3);
                 atomicAdd(p.segments + 36 + kMaxBounceCounters, (unsigned long long)f1);
-                atomicAdd(p.segments + 37 + kMaxBounceCounters, (unsigned long long)(64 - f7 - f0 - f3 - f1));
+                atomicAdd(p.segments + 37 + kMaxBounceCounters, (unsigned long long)(64 - f0 - f3 - f1));
                 atomicAdd(p.segments + 38 + kMaxBounceCounters, exhausted ? 1ull : 0ull);
             }
             break;
@@ -1844,12 +1838,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (c4 * 4 > cm * PT_LEAF_W) { phase = 4; cm = c4; }
             if (c5 * 4 > cm * PT_WALK_W) { phase = 8; cm = c5; }
             if (c1 * 4 > cm * PT_SEL_W) { phase = 1; cm = c1; }
-            if (kFullLater) {
-                // fast-certificate failures wait in state 7 for a batch of the full certificate:
-                // run it once kFullBatch of them are waiting, or when nothing else is left
-                const int c7 = __popcll(__ballot(state == 7));
-                if (c7 >= kFullBatch || (c7 > 0 && c1 + c2 + c4 + c5 == 0)) phase = 32;
-            }
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
@@ -2047,8 +2035,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
-        } else if (((phase & 8) && state == 5) || (kFullLater && (phase & 32) && state == 7)) {
-            // the walk: certificate, else the exact walk (phase 32: the batched full certificate)
+        } else if ((phase & 8) && state == 5) {          // the walk: certificate, else the exact walk
             if (PT_TRACE_STATS && (p.debug & 2048))       // walks by hit-set size: 1, 2, 3, >= 4 (pool: >= 4)
                 atomicAdd(p.segments + 51 + (pblk >= 0 ? 3 : min(nh, 4) - 1) + kMaxBounceCounters, 1ull);
             const ModelRec& M = models[im];
@@ -2073,30 +2060,27 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 bool ok = false;
                 // ninv (1/d clamped to +-1e30, set at select) is the exact 1/d when no slope is clamped
                 const bool exact_inv = (absr(ninv.x) < 1e30f) & (absr(ninv.y) < 1e30f) & (absr(ninv.z) < 1e30f);
-                if (PT_CERT_MODE >= 1 && pblk < 0 && exact_inv && !(phase & 32))
+                if (PT_CERT_MODE >= 1 && pblk < 0 && exact_inv)
                     ok = walk_certify_fast<kGfHitCap>(p, M, d, ninv, pt, t_box, lds_get, nh, tmin, win, tri);
                 if (PT_TRACE_STATS && (p.debug & 4)) {
                     atomicAdd(p.segments + 42 + kMaxBounceCounters, 1ull);
                     if (ok) atomicAdd(p.segments + 40 + kMaxBounceCounters, 1ull);
                 }
-                if (PT_CERT_MODE <= 1 && !ok && pblk < 0 && (!kFullLater || (phase & 32))) {
+                if (PT_CERT_MODE <= 1 && !ok && pblk < 0) {
                     const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                     ok = walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, lds_get, nh, tmin, win, tri);
                     if (PT_TRACE_STATS && (p.debug & 4) && ok) atomicAdd(p.segments + 41 + kMaxBounceCounters, 1ull);
                 }
                 w.hit = ok; w.has_best = ok; w.final_min = ok; w.t = tmin; w.tri = tri; w.tw = 0.0f;
-                // a fast-certificate failure waits for the batched full certificate (state 7);
-                // a full-certificate failure, or a pool hit set, is handed on (state 6); a
-                // certified ray (5, also out of state 7) takes the result handling below
-                state = ok ? 5 : (kFullLater && !(phase & 32) && pblk < 0) ? 7 : 6;
+                if (!ok) state = 6;
             } else {
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
                              : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
                                                     tmin, win);
             }
-            if (state == 6 || state == 7) {
-                // handed on below (6), or waiting for the batched full certificate (7)
+            if (state == 6) {
+                // handed on below
             } else if (tier == 2 || w.final_min || w.tw < tmin + win) {
                 if (w.hit && w.has_best) {
                     const float dd = model_hit_dist(M, o, d, w.t, ow);
@@ -2112,7 +2096,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[4] += t - ts; ts = t; }
-        if ((phase & 16) || (!TAIL && (phase & 40) && __ballot(state == 6))) {
+        if ((phase & 16) || (!TAIL && (phase & 8) && __ballot(state == 6))) {
             if (PT_TRACE_STATS && (p.debug & 32) && lane == 0)     // walk iterations with hand-ons, drains
                 atomicAdd(p.segments + ((phase & 16) ? 27 : 26) + kMaxBounceCounters, 1ull);
             // hand-on records: the drain (phase 16: every busy lane's exact state, then
@@ -2134,7 +2118,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (mine) {
                 int* C = cout + (drain ? r : p.cont_cap - 1 - r);
                 const size_t cs = (size_t)p.cont_cap;
-                C[kCJ * cs] = j; C[kCState * cs] = (drain && state != 7) ? state : 5; C[kCIm * cs] = im;
+                C[kCJ * cs] = j; C[kCState * cs] = drain ? state : 5; C[kCIm * cs] = im;
                 C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
                 C[kCOw * cs] = __float_as_int(ow.x); C[(kCOw + 1) * cs] = __float_as_int(ow.y);
                 C[(kCOw + 2) * cs] = __float_as_int(ow.z);
