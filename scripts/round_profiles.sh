@@ -2,6 +2,7 @@
 #   - rocprofv3 --kernel-trace --stats of the bench command at its 16 pipelines and at 1
 #   - FETCH_SIZE / WRITE_SIZE passes (one pipeline: PMC collection serialises dispatches)
 #   - SQ_INSTS_VALU / SQ_INSTS_SALU passes at 16 pipelines and at 1
+#   - an SQ wave-cycle pass (waits, issue, VALU lanes), one pipeline
 #   - rocprofv3 --kernel-trace --stats of the north_star target (1M triangles) and of
 #     configs[4] (10M triangles, 16 bounces, scene built in memory), 16 pipelines
 # then scripts/pmc_summary.py folds the counters into gpurun_out/pmc_round.json
@@ -32,4 +33,9 @@ for s in 1 2 3 4 11 12; do
   f=$(find gpurun_out/s${s}_prof -name "*kernel_stats.csv" | head -1)
   cp "$f" gpurun_out/round/kernel_stats_s$s.csv
 done
+# wave-cycle split of the traces (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES) and
+# VALU lane use (THREAD_CYCLES_VALU / ACTIVE_INST_VALU / 64), one pipeline: gpurun_out/s1_counters.txt
+bash scripts/gpu_run.sh \
+  "counters=SQ_WAVES,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_THREAD_CYCLES_VALU,SQ_INSTS_VALU@$B $S --pipelines 1" || exit $?
+python3 scripts/pmc_table.py gpurun_out/s1_counters > gpurun_out/round/sq_cycles_p1.txt || exit 1
 echo "profiles: gpurun_out/round/ (s1 grid_fast 16p, s2 grid_fast 1p, s3 bvh 16p, s4 bvh 1p, s11 1M tris, s12 10M tris), $O"
