@@ -50,6 +50,9 @@ constexpr int kBlock = 256;
 #ifndef PT_MINWAVES
 #define PT_MINWAVES 5
 #endif
+#ifndef PT_NODE_STEP
+#define PT_NODE_STEP 6        // k_trace_gf: node visits per node step (lanes still at an inner node go on)
+#endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
 constexpr int kSortBits = 12, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
@@ -1254,6 +1257,9 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
 #ifndef PT_LEAF_STEP
 #define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of k_trace_bvh (1..4; k_trace_gf: 1 or 2)
 #endif
+#ifndef PT_BVH_NODE_STEP
+#define PT_BVH_NODE_STEP 1    // k_trace_bvh: node visits per node step (as PT_NODE_STEP)
+#endif
 #ifndef PT_BVH_LEAF_W
 #define PT_BVH_LEAF_W 4       // k_trace_bvh phase weights (x/4) of leaf and select lane counts against node's
 #endif
@@ -1535,9 +1541,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 sp -= pop ? 1 : 0;
             }
         } else if ((phase & 2) && state == 2) {
-            {
-                // node visit; hit leaf children become pending leaves (tested one
-                // triangle per iteration, in the order bvh_step tests them)
+#pragma unroll 1
+            for (int ks = 0; ks < PT_BVH_NODE_STEP; ks++) {
+                // node visits (lanes still at an inner node go on); hit leaf children become
+                // pending leaves (tested in the order bvh_step tests them)
                 const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
                 const float4 q0 = nodes[4 * cur + 0];
                 const float4 q1 = nodes[4 * cur + 1];
@@ -1573,6 +1580,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
                 lf_next = leaf ? next : lf_next;
                 state = leaf ? 4 : state;
+                if (state != 2 || model_done) break;
             }
         }
         if (model_done) {
@@ -1977,47 +1985,51 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 state = (tonext | pop) ? 2 : state;
                 sp -= pop ? 1 : 0;
             }
-        } else if ((phase & 2) && state == 2) {         // one node of the collection (window t_min + win)
-            const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-            const float4 q0 = nodes[4 * cur + 0];
-            const float4 q1 = nodes[4 * cur + 1];
-            const float4 q2 = nodes[4 * cur + 2];
-            const float4 q3 = nodes[4 * cur + 3];
-            const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-            const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-            const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-            const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-            float tn0, tf0, tn1, tf1, tx0, tx1;
-            node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
-            node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
-            const float X = tmin + win;
-            const float bound = X + gf_slack(X, t_box);
-            // non-short-circuit: both children's slabs in one basic block (a branch on
-            // cnt >= 0 moved the float work into its own block, where every min/max
-            // operand was re-canonicalised)
-            const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
-            const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
-            // the step's decisions as selects; only the push and the pop touch memory
-            // (the traces are issue-bound: every divergent branch costs scalar exec-mask work)
-            const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
-            const bool i0 = h0 & (cnt0 == 0), i1 = h1 & (cnt1 == 0);
-            const bool both = i0 & i1;
-            const bool first0 = tn0 <= tn1;             // near child first tightens the bound
-            const int next = both ? (first0 ? link0 : link1) : (i0 ? link0 : (i1 ? link1 : -1));
-            if (both) spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, first0 ? link1 : link0);
-            sp += both ? 1 : 0;
-            const bool leaf = l0 | l1;                  // leaf 0, then leaf 1, then `next`
-            const bool pop = !leaf & (next < 0) & (sp > 0);
-            const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
-            collected = !leaf & (next < 0) & (sp == 0);
-            sp -= pop ? 1 : 0;
-            cur = leaf ? cur : (next >= 0 ? next : (pop ? top : cur));
-            lf_i = leaf ? (l0 ? link0 : link1) : lf_i;
-            lf_e = leaf ? lf_i + (l0 ? cnt0 : cnt1) : lf_e;
-            lf2_i = leaf ? ((l0 & l1) ? link1 : 0) : lf2_i;
-            lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
-            lf_next = leaf ? next : lf_next;
-            state = leaf ? 4 : state;
+        } else if ((phase & 2) && state == 2) {         // PT_NODE_STEP nodes of the collection (window t_min + win)
+#pragma unroll 1
+            for (int ks = 0; ks < PT_NODE_STEP; ks++) {
+                const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
+                const float4 q0 = nodes[4 * cur + 0];
+                const float4 q1 = nodes[4 * cur + 1];
+                const float4 q2 = nodes[4 * cur + 2];
+                const float4 q3 = nodes[4 * cur + 3];
+                const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
+                const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
+                const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
+                const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
+                float tn0, tf0, tn1, tf1, tx0, tx1;
+                node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
+                node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
+                const float X = tmin + win;
+                const float bound = X + gf_slack(X, t_box);
+                // non-short-circuit: both children's slabs in one basic block (a branch on
+                // cnt >= 0 moved the float work into its own block, where every min/max
+                // operand was re-canonicalised)
+                const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
+                const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
+                // the step's decisions as selects; only the push and the pop touch memory
+                // (the traces are issue-bound: every divergent branch costs scalar exec-mask work)
+                const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
+                const bool i0 = h0 & (cnt0 == 0), i1 = h1 & (cnt1 == 0);
+                const bool both = i0 & i1;
+                const bool first0 = tn0 <= tn1;             // near child first tightens the bound
+                const int next = both ? (first0 ? link0 : link1) : (i0 ? link0 : (i1 ? link1 : -1));
+                if (both) spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, first0 ? link1 : link0);
+                sp += both ? 1 : 0;
+                const bool leaf = l0 | l1;                  // leaf 0, then leaf 1, then `next`
+                const bool pop = !leaf & (next < 0) & (sp > 0);
+                const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
+                collected = !leaf & (next < 0) & (sp == 0);
+                sp -= pop ? 1 : 0;
+                cur = leaf ? cur : (next >= 0 ? next : (pop ? top : cur));
+                lf_i = leaf ? (l0 ? link0 : link1) : lf_i;
+                lf_e = leaf ? lf_i + (l0 ? cnt0 : cnt1) : lf_e;
+                lf2_i = leaf ? ((l0 & l1) ? link1 : 0) : lf2_i;
+                lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
+                lf_next = leaf ? next : lf_next;
+                state = leaf ? 4 : state;
+                if (state != 2 || collected) break;    // a leaf reached, or the collection done
+            }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
         if (collected) {
