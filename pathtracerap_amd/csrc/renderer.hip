@@ -1258,7 +1258,7 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
 #define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of k_trace_bvh (1..4; k_trace_gf: 1 or 2)
 #endif
 #ifndef PT_BVH_NODE_STEP
-#define PT_BVH_NODE_STEP 1    // k_trace_bvh: node visits per node step (as PT_NODE_STEP)
+#define PT_BVH_NODE_STEP 4    // k_trace_bvh: node visits per node step (as PT_NODE_STEP)
 #endif
 #ifndef PT_BVH_LEAF_W
 #define PT_BVH_LEAF_W 4       // k_trace_bvh phase weights (x/4) of leaf and select lane counts against node's
