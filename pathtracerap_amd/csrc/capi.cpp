@@ -1,13 +1,17 @@
 // capi.cpp -- extern "C" boundary (include/pathtracer_amd.h).
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/pathtracer_amd.h"
 #include "renderer.h"
 #include "scene.h"
 
-struct pt_scene { pt::Scene s; };
+// bvh_mu: pt_renderer_allocate_on_gpu may add the BLAS to a scene built grid-only;
+// renderers allocating from one shared scene on several threads (ctypes drops the
+// GIL) take turns there, and only the first one builds
+struct pt_scene { pt::Scene s; std::mutex bvh_mu; };
 struct pt_renderer { pt::Renderer* r; };
 
 static thread_local std::string g_err;
@@ -219,12 +223,13 @@ int pt_renderer_bind_image(pt_renderer* r, float* d) { R_CALL(r->r->bindImage(d)
 int pt_renderer_allocate_on_gpu(pt_renderer* r, const pt_scene* s) {
     if (!s) return set_err("null scene");
     if (!r || !r->r) return set_err("null renderer");
-    if (r->r->cfg.accel != PT_ACCEL_GRID && s->s.built && s->s.bvh_nodes.empty()) {
-        // grid_fast / bvh traverse the per-mesh BLAS: a scene built grid-only gets it
-        // here, once (the scene's grid tables are rebuilt identically alongside)
-        pt::Scene& S = const_cast<pt_scene*>(s)->s;
-        if (S.ensureBvh() < 0) return set_err(S.last_error);
-    }
+    // grid_fast / bvh traverse the per-mesh BLAS: a scene built grid-only gets it here,
+    // once (the scene's grid tables are rebuilt identically alongside); the lock also
+    // keeps other renderers from reading the scene while that happens
+    pt_scene* ms = const_cast<pt_scene*>(s);
+    std::lock_guard<std::mutex> lock(ms->bvh_mu);
+    if (r->r->cfg.accel != PT_ACCEL_GRID && ms->s.built && ms->s.bvh_nodes.empty() && ms->s.ensureBvh() < 0)
+        return set_err(ms->s.last_error);
     R_CALL(r->r->allocateOnGPU(s->s));
 }
 int pt_renderer_clear_image(pt_renderer* r) { R_CALL(r->r->clearImage()); }

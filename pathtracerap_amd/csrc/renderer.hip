@@ -2696,7 +2696,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const bool spills = split_trace && cfg.accel == ACCEL_GRID_FAST;   // k_trace_gf's 12-entry LDS stack
         // drain continuations
         const char* dd = std::getenv("PT_DRAIN_DUMP");
-        kp.drain_dump = split_trace ? std::max(0, std::min(64, dd ? std::atoi(dd) : 32)) : 0;
+        kp.drain_dump = split_trace ? std::max(0, std::min(64, dd ? std::atoi(dd) : 16)) : 0;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
         // walk hand-ons (k_trace_gf main launch -> its level-1 tail): room for one per lane
         // (PT_WALK_WCAP overrides; beyond it a ray goes whole to k_trace_deferred).  With one

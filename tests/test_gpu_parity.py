@@ -50,3 +50,24 @@ def test_render_reference_scene_bitexact(gpu, pt_mod, oracle_mod, accel):
     oimg, oseg = O.render(flat_from_export(s.export()), oracle_cfg(cfg))
     assert seg == oseg
     assert_bitexact(img, oimg, "image")
+
+
+def test_grid_only_scene_shared_by_three_renderers(gpu, pt_mod, oracle_mod):
+    """A scene built grid-only (build(bvh=False)) and shared by renderers of all three
+    modes, allocated from three threads at once (ctypes drops the GIL): the first
+    grid_fast / bvh allocation adds the BLAS under the scene's lock
+    (capi.cpp pt_renderer_allocate_on_gpu), and every image still equals the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+    P, O = pt_mod, oracle_mod
+    s = _ref_scene(P, bvh=False)
+    rs = [P.Renderer(P.RenderConfig(width=160, height=128, iterations=2, accel=a)) for a in (2, 1, 0)]
+    with ThreadPoolExecutor(3) as ex:
+        list(ex.map(lambda r: r.allocateOnGPU(s), rs))
+    flat = flat_from_export(s.export())
+    for r in rs:
+        r.renderLoop()
+        img, seg = r.image(), r.segments()
+        oimg, oseg = O.render(flat, oracle_cfg(r.cfg))
+        r.free()
+        assert seg == oseg
+        assert_bitexact(img, oimg, "image")
