@@ -859,27 +859,31 @@ __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelR
             ax = (lb | ha) ? a : ax;
             below = (lb | ha) ? lb : below;
         }
-        // one extension: only the part of h's box outside m*'s along axis ax can hold a
-        // voxel the walk visits before m*'s box
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            const bool cut = (ext == 1) & (a == ax);
-            mh[a] = (cut & below) ? bl[a] - 1 : mh[a];
-            ml[a] = (cut & !below) ? bh[a] + 1 : ml[a];
-        }
-        float g = -3.0e38f, go = 3.0e38f;
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            const float L = M.bbox[a] + (float)ml[a] * M.vw[a] - dl[a];
-            const float H = M.bbox[a] + (float)(mh[a] + 1) * M.vw[a] + dl[a];
-            const float s0 = (L - pp[a]) * iv[a], s1 = (H - pp[a]) * iv[a];
-            g = fmaxf(g, fminf(s0, s1));
-            go = fminf(go, fmaxf(s0, s1));
-        }
+        // m* itself, a member inside m*'s box, or a start inside B*: nothing to test
+        // (a branch, not a select: the common single-member hit set skips the float work)
         const bool mn = __int_as_float(m.x) == tmin;
-        const bool missed = (g > go + 1e-5f * (absr(go) + 1.0f)) & (absr(g) < 1e30f);
-        const bool after = (g - 1e-5f * (absr(g) + 1.0f) > ss) & (absr(g) < 1e30f);
-        ok = ok & (mn | (ext == 0) | start_in | missed | after);
+        if (!(mn | (ext == 0) | start_in)) {
+            // one extension: only the part of h's box outside m*'s along axis ax can hold a
+            // voxel the walk visits before m*'s box
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const bool cut = (ext == 1) & (a == ax);
+                mh[a] = (cut & below) ? bl[a] - 1 : mh[a];
+                ml[a] = (cut & !below) ? bh[a] + 1 : ml[a];
+            }
+            float g = -3.0e38f, go = 3.0e38f;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const float L = M.bbox[a] + (float)ml[a] * M.vw[a] - dl[a];
+                const float H = M.bbox[a] + (float)(mh[a] + 1) * M.vw[a] + dl[a];
+                const float s0 = (L - pp[a]) * iv[a], s1 = (H - pp[a]) * iv[a];
+                g = fmaxf(g, fminf(s0, s1));
+                go = fminf(go, fmaxf(s0, s1));
+            }
+            const bool missed = (g > go + 1e-5f * (absr(go) + 1.0f)) & (absr(g) < 1e30f);
+            const bool after = (g - 1e-5f * (absr(g) + 1.0f) > ss) & (absr(g) < 1e30f);
+            ok = ok & (missed | after);
+        }
     }
     tri = ms_y;
     return ok;

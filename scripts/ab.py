@@ -125,6 +125,9 @@ def main():
                                                         "margin", "not_in_Bstar", "window"],
                                                        [round(c / max(rs[v].segments(), 1), 4) for c in cf]))
             out[v]["cert_ok_per_segment"] = round(allc[76] / max(rs[v].segments(), 1), 4)
+        wb = allc[114:118]                             # slots 51..54: walks by hit-set size 1, 2, 3, >= 4
+        if any(wb):
+            out[v]["walks_by_hitset_size"] = dict(zip(["1", "2", "3", ">=4"], [round(c / max(sum(wb), 1), 3) for c in wb]))
         diag = allc[64:67]
         if any(diag):
             out[v]["diag_tier2_t1overflow_fallback"] = diag
