@@ -38,6 +38,29 @@ def test_trace_iteration_cap_is_an_error(gpu, pt_mod, synth_dir, monkeypatch, ac
     r.free()
 
 
+def test_trace_fault_records_the_stuck_lanes(gpu, pt_mod, synth_dir, monkeypatch):
+    """A k_trace_gf wave that gives up records its 64 lanes by state in diagnostic
+    slots 34..37 (idle, done, select, node/leaf/walk) and counts itself in 38 when its
+    ray pool was exhausted (renderer.hip, the iteration-cap check): scripts/hangcheck.py
+    prints them, which is how the state-7 livelock of round 4 was found."""
+    P = pt_mod
+    monkeypatch.setenv("PT_TRACE_ITER_CAP", "3")
+    s = _scene(P, synth_dir)
+    r = P.Renderer(P.RenderConfig(width=64, height=48, iterations=1, max_bounces=4, accel=P.ACCEL_GRID_FAST,
+                                  pipelines=2))
+    r.allocateOnGPU(s)
+    r.renderLoop(0, 2, sync=False)
+    with pytest.raises(P.PathTracerError, match="gave up"):
+        r.synchronize()
+    faults = r.trace_faults()
+    v = r.segments_per_bounce(128)
+    lanes = [v[63 + slot] for slot in range(34, 38)]
+    assert faults > 0
+    assert sum(lanes) == 64 * faults, (lanes, faults)
+    assert 0 <= v[63 + 38] <= faults
+    r.free()
+
+
 @pytest.mark.parametrize("accel", [1, 2])
 def test_no_trace_faults_in_a_normal_run(gpu, pt_mod, synth_dir, accel):
     P = pt_mod

@@ -455,7 +455,7 @@ def test_graph_replay_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypa
 
 
 @pytest.mark.parametrize("accel", [1, 2])
-@pytest.mark.parametrize("dump,levels", [(0, 1), (1, 1), (32, 1), (64, 1), (32, 4), (64, 2)])
+@pytest.mark.parametrize("dump,levels", [(0, 1), (1, 1), (8, 1), (16, 1), (32, 1), (64, 1), (16, 2), (32, 4), (64, 2)])
 @pytest.mark.parametrize("scene", ["synthetic", "reference"])
 def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, dump, levels, scene):
     """PT_DRAIN_DUMP: waves of a persistent trace whose pool is exhausted hand
