@@ -50,6 +50,9 @@ constexpr int kBlock = 256;
 #ifndef PT_MINWAVES
 #define PT_MINWAVES 5
 #endif
+#ifndef PT_SEL_MASK
+#define PT_SEL_MASK 1         // k_trace_gf main launch: select steps jump over models a fresh ray's mask rules out
+#endif
 #ifndef PT_NODE_STEP
 #define PT_NODE_STEP 6        // k_trace_gf: node visits per node step (lanes still at an inner node go on)
 #endif
@@ -1685,6 +1688,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     __shared__ int4 s_hs[kGfHitCap * BS];
     constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModelsGf) : 1;
     __shared__ ModelRec s_models[kModelsHere];
+    // PT_SEL_MASK: per lane, the models whose world box the ray can reach (gdist aside),
+    // found once per ray so later select steps jump to the next candidate
+    constexpr bool kSelMask = PT_SEL_MASK && !TAIL && (F & 1);
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
@@ -1725,6 +1731,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
     bool exhausted = false;
+    unsigned cmask = 0;                            // PT_SEL_MASK: candidate models of the lane's ray
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
     unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_walk = 0, it_sel = 0;
@@ -1872,15 +1879,40 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             // rare) instead of living in registers through the traversal
             const f3 winv = node_inv(cull_inv(dw));
             const float dlen = sqrtf(dot(dw, dw));
+            if (kSelMask) {
+                if (im < 0) {                               // a fresh ray: every model's miss test, once
+                    cmask = 0;
+                    for (int m = 0; m < p.nmodels; m++) {
+                        const ModelRec& M = models[m];
+                        float wtn, wtf;
+                        node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
+                        bool cand = !((wtn > wtf) | (wtf * dlen < -1.0f));
+                        if (!cand) {                        // model_culled's zero-slope exception
+                            const f3 dm = xform12(M.w2m, dw, 0.0f);
+                            cand = !(dm.x != 0.0f && dm.y != 0.0f && dm.z != 0.0f);
+                        }
+                        cmask |= cand ? 1u << m : 0u;
+                    }
+                }
+            }
             for (;;) {
-                im++;
+                if (kSelMask) {                             // the next candidate model
+                    const unsigned rest = cmask >> (im + 1);
+                    im = rest ? im + __ffs(rest) : p.nmodels;
+                } else {
+                    im++;
+                }
                 if (im >= p.nmodels) {
                     put_hit(p, j, gdist, gmodel, gtri);
                     state = 0;
                     break;
                 }
                 const ModelRec& M = models[im];
-                if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (kSelMask) {                             // model_culled's gdist test for a candidate
+                    float wtn, wtf;
+                    node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
+                    if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;
+                } else if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
