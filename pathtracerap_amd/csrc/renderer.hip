@@ -1267,6 +1267,9 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
 #ifndef PT_BVH_NODE_STEP
 #define PT_BVH_NODE_STEP 4    // k_trace_bvh: node visits per node step (as PT_NODE_STEP)
 #endif
+#ifndef PT_BVH_SEL_MASK
+#define PT_BVH_SEL_MASK 1     // k_trace_bvh: PT_SEL_MASK's candidate mask for the main launch's select steps
+#endif
 #ifndef PT_BVH_LEAF_W
 #define PT_BVH_LEAF_W 4       // k_trace_bvh phase weights (x/4) of leaf and select lane counts against node's
 #endif
@@ -1358,6 +1361,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
     bool any = false, exhausted = false;
+    // PT_BVH_SEL_MASK: the main launch's select steps jump to the next model a ray can reach
+    // (k_trace_gf's PT_SEL_MASK; the miss test once per ray, the gdist test per candidate)
+    constexpr bool kSelMask = PT_BVH_SEL_MASK && !TAIL && (F & 1);
+    unsigned cmask = ~0u;
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
     unsigned long long st_busy = 0, st_drain = 0, st_drain_busy = 0;       // busy lanes; iterations after exhaustion
     unsigned long long it_node = 0, it_leaf = 0, it_sel = 0;
@@ -1422,6 +1429,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         winv = node_inv(cull_inv(dw));
                         dlen = sqrtf(dot(dw, dw));
                         gdist = kFMax; gmodel = -1; gtri = -1; im = -1;
+                        cmask = ~0u;
                         state = 1;
                     } else {
                         state = 3;
@@ -1488,15 +1496,32 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             state = 3;
         }
         if ((phase & 1) && state == 1) {                // advance to the next model that survives culling
+            if (kSelMask && cmask == ~0u) {
+                cmask = 0;
+                for (int m = 0; m < p.nmodels; m++) {
+                    float wtn, wtf;
+                    node_slab(models[m].wbox, models[m].wbox + 3, ow, winv, wtn, wtf);
+                    cmask |= ((wtn > wtf) | (wtf * dlen < -1.0f)) ? 0u : 1u << m;
+                }
+            }
             for (;;) {
-                im++;
+                if (kSelMask) {
+                    const unsigned rest = cmask >> (im + 1);
+                    im = rest ? im + __ffs(rest) : p.nmodels;
+                } else {
+                    im++;
+                }
                 if (im >= p.nmodels) {
                     put_hit(p, j, gdist, gmodel, gtri);
                     state = 0;
                     break;
                 }
                 const ModelRec& M = models[im];
-                if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (kSelMask) {
+                    float wtn, wtf;
+                    node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
+                    if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;
+                } else if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
