@@ -53,8 +53,11 @@ constexpr int kBlock = 256;
 #ifndef PT_SEL_MASK
 #define PT_SEL_MASK 1         // k_trace_gf main launch: select steps jump over models a fresh ray's mask rules out
 #endif
+#ifndef PT_NODE_MINLANES
+#define PT_NODE_MINLANES 8    // k_trace_gf: the wave leaves a node step once fewer lanes than this are still at a node
+#endif
 #ifndef PT_NODE_STEP
-#define PT_NODE_STEP 6        // k_trace_gf: node visits per node step (lanes still at an inner node go on)
+#define PT_NODE_STEP 8        // k_trace_gf: node visits per node step (lanes still at an inner node go on)
 #endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
 constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
@@ -2090,6 +2093,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 lf_next = leaf ? next : lf_next;
                 state = leaf ? 4 : state;
                 if (state != 2 || collected) break;    // a leaf reached, or the collection done
+                // PT_NODE_MINLANES: the whole wave leaves the step once few lanes are still at a node
+                if (PT_NODE_MINLANES > 0 && __popcll(__ballot(state == 2 && !collected)) < PT_NODE_MINLANES) break;
             }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
