@@ -1719,6 +1719,11 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     // PT_SEL_MASK: per lane, the models whose world box the ray can reach (gdist aside),
     // found once per ray so later select steps jump to the next candidate
     constexpr bool kSelMask = PT_SEL_MASK && !TAIL && (F & 1);
+    // node steps: the in-place variant (F & 16: one pipeline, one launch alone on the chip)
+    // measured best at 6 visits without the minimum (0.537 vs 0.558 ms per launch); the
+    // hand-on variants of several pipelines at PT_NODE_STEP / PT_NODE_MINLANES
+    constexpr int kNodeSteps = (F & 16) ? 6 : PT_NODE_STEP;
+    constexpr int kNodeMinLanes = (F & 16) ? 0 : PT_NODE_MINLANES;
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
@@ -2051,7 +2056,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
         } else if ((phase & 2) && state == 2) {         // PT_NODE_STEP nodes of the collection (window t_min + win)
 #pragma unroll 1
-            for (int ks = 0; ks < PT_NODE_STEP; ks++) {
+            for (int ks = 0; ks < kNodeSteps; ks++) {
                 const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
                 const float4 q0 = nodes[4 * cur + 0];
                 const float4 q1 = nodes[4 * cur + 1];
@@ -2094,7 +2099,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 state = leaf ? 4 : state;
                 if (state != 2 || collected) break;    // a leaf reached, or the collection done
                 // PT_NODE_MINLANES: the whole wave leaves the step once few lanes are still at a node
-                if (PT_NODE_MINLANES > 0 && __popcll(__ballot(state == 2 && !collected)) < PT_NODE_MINLANES) break;
+                if (kNodeMinLanes > 0 && __popcll(__ballot(state == 2 && !collected)) < kNodeMinLanes) break;
             }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
