@@ -247,21 +247,54 @@ def load_sq(workload_key, tag="_sq"):
 
 
 class Ctx:
-    """Process-group plumbing shared by every timed workload."""
+    """Process-group plumbing shared by every timed workload.  ``pg``: a process
+    group exists (a launcher or bench.py's own spawner set WORLD_SIZE, also at
+    world size 1), so the accumulator all-reduce and the max-over-ranks run through
+    it exactly as on N GPUs."""
 
-    def __init__(self, torch, dist, dev, rank, world):
-        self.torch, self.dist, self.dev, self.rank, self.world = torch, dist, dev, rank, world
+    def __init__(self, torch, dist, dev, rank, world, pg=False):
+        self.torch, self.dist, self.dev, self.rank, self.world, self.pg = torch, dist, dev, rank, world, pg
 
     def barrier(self):
-        if self.world > 1:
+        if self.pg:
             self.dist.barrier()
 
     def reduce(self, vals, op):
         """vals (floats) reduced over ranks with op ('max' / 'sum')."""
         t = self.torch.tensor(vals, dtype=self.torch.float64, device=self.dev)
-        if self.world > 1:
+        if self.pg:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
         return [float(x) for x in t.cpu()]
+
+
+def check_backend(backend, world, ngpu):
+    """RCCL needs one GPU per rank: more ranks than visible GPUs would map two
+    ranks onto one device, and init_process_group then fails or hangs.  Checked
+    before any process-group or GPU call; returns an error string or None."""
+    if backend == "nccl" and world > ngpu:
+        return (f"bench: --dist-backend nccl with {world} rank(s) but {ngpu} visible GPU(s); RCCL needs one "
+                f"GPU per rank (use --dist-backend gloo to rehearse several ranks on one GPU)")
+    return None
+
+
+def bound_fracs(obj, path="line"):
+    """Every ``frac`` in the line is a fraction of a hardware peak: one above 1
+    (or not finite) is a measurement error, so it is published as null beside an
+    ``error`` key instead of as a number.  Returns the paths it nulled."""
+    bad = []
+    if isinstance(obj, dict):
+        for k, v in list(obj.items()):
+            if k == "frac" and v is not None:
+                if not (isinstance(v, (int, float)) and 0.0 <= v <= 1.0):
+                    obj["frac"] = None
+                    obj["error"] = f"frac {v!r} outside [0, 1]: inconsistent counters, not published"
+                    bad.append(path)
+            else:
+                bad += bound_fracs(v, f"{path}.{k}")
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            bad += bound_fracs(v, f"{path}[{i}]")
+    return bad
 
 
 def timed_run(P, ctx, scene, cfg, K, W, iter_base, reduce_image, full_spp=0):
@@ -284,7 +317,7 @@ def timed_run(P, ctx, scene, cfg, K, W, iter_base, reduce_image, full_spp=0):
     r.renderLoop(first_iter=iter_base + rank * max(W, 1), n_iters=W, sync=False)
     torch.cuda.synchronize(dev)
     faults = r.trace_faults()          # clearImage resets the counter: read the warmup's first
-    if reduce_image and world > 1:
+    if reduce_image and ctx.pg:
         # warm the accumulator-sized all-reduce: one-time RCCL setup is paid here
         ctx.dist.all_reduce(image, op=ctx.dist.ReduceOp.SUM)
         torch.cuda.synchronize(dev)
@@ -295,7 +328,7 @@ def timed_run(P, ctx, scene, cfg, K, W, iter_base, reduce_image, full_spp=0):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         r.renderLoop(first_iter=first, n_iters=n, sync=False)
-        if reduce_image and world > 1:
+        if reduce_image and ctx.pg:
             ctx.dist.all_reduce(image, op=ctx.dist.ReduceOp.SUM)      # RCCL over xGMI
         torch.cuda.synchronize(dev)
         ctx.barrier()
@@ -379,6 +412,69 @@ def one_pipeline_pass(P, torch, dev, scene, cfg, K, W):
     return st
 
 
+def target_key(accel, name, cfg):
+    """pmc_latest.json key of a target workload: the key its own main-line run
+    (bench.py --ntri N --bounces B [--inmem]) writes, so scripts/round_profiles.sh's
+    per-target counter passes line up with the targets' one-pipeline passes."""
+    ntri = {"target_1m": 1_000_000, "configs4": 10_000_000}.get(name)
+    if ntri is None:
+        return f"{accel}_{name}_{cfg.width}x{cfg.height}_b{cfg.max_bounces}"
+    return f"{accel}_{ntri}_{cfg.width}x{cfg.height}_b{cfg.max_bounces}"
+
+
+def trace_roofline(stats1, per_bounce, K, elapsed, ms_per_step, kname, workload_key):
+    """Roofline of the dominant kernel, the persistent trace of bounces >= 1
+    (k_trace_gf / k_trace_bvh), per launch.  Algorithmic bytes per segment
+    entering bounce b >= 1: 32 B ray read (o, d) + 20 B hit record write; one
+    "launch" = one bounce's trace phase, timed by a HIP event pair on the stream
+    it is launched on, with one pipeline (no overlap, no drain tail).  Beside it:
+    the PMC HBM bytes of the same launches (traffic), their VALU issue rate and
+    the wave-cycle split, all from profiles/pmc_latest.json under workload_key."""
+    if not stats1 or stats1.get("trace_launches", 0) <= 0:
+        return None
+    tb_step = trace_bytes_per_step(per_bounce, K)
+    phases = max(1, len(per_bounce) - 1)                 # trace phases per step
+    b_launch = tb_step / phases                          # algorithmic bytes per launch (one bounce's trace)
+    job = tb_step / (elapsed / K) / 1e9                  # per GPU: each rank runs K steps
+    l1 = stats1["trace_launches"]
+    k1 = stats1["trace_ms"] / l1
+    a1 = b_launch / (k1 / 1e3) / 1e9
+    tr = load_pmc(kname, workload_key)                   # PMC HBM bytes per launch, one pipeline
+    roof = {"bound": "hbm", "achieved": round(a1, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(a1 / HBM_PEAK_GBS, 5), "traffic": None if tr is None else round(tr),
+            "kernel": kname, "workload_key": workload_key,
+            "basis": "per launch: algorithmic bytes of one bounce's trace (52 B x segments entering the bounce) "
+                     "/ its average duration, HIP events on the launch stream, one pipeline (rocprofv3: "
+                     "profiles/r05/kernel_stats_*_1p.csv); traffic = PMC HBM bytes per launch of the same "
+                     "command, (2 FETCH_SIZE + WRITE_SIZE) KiB (profiles/pmc_latest.json)",
+            "algorithmic_bytes_per_launch": round(b_launch), "avg_launch_ms": round(k1, 4),
+            "launches": l1, "trace_phases_per_step": phases,
+            "per_step": {"achieved": round(job, 2), "frac": round(job / HBM_PEAK_GBS, 5),
+                         "algorithmic_bytes_per_step": round(tb_step), "ms_per_step": ms_per_step,
+                         "note": "whole-job rate: algorithmic trace bytes per step / ms_per_step (the iterations "
+                                 "in flight share the step's wall time)"},
+            "sort_avg_ms": round(stats1["sort_ms"] / max(stats1["sort_launches"], 1), 4),
+            "shade_avg_ms": round(stats1["bounce_ms"] / max(stats1["bounce_launches"], 1), 4),
+            "scan_avg_ms": round(stats1["scan_ms"] / max(stats1["scan_launches"], 1), 4)}
+    if tr is not None:
+        roof["traffic_over_algorithmic"] = round(tr / max(b_launch, 1.0), 2)
+    sq1 = load_sq(workload_key, "_sq_p1")
+    kv = (sq1 or {}).get("kernels", {}).get(kname)
+    if kv:
+        g = kv["valu_insts_per_launch"] / (k1 / 1e3) / 1e9
+        roof["issue"] = {"bound": "valu", "unit": "G wave-instr/s", "peak": VALU_PEAK_G,
+                         "valu_insts_per_launch": round(kv["valu_insts_per_launch"]),
+                         "achieved": round(g, 1), "frac": round(g / VALU_PEAK_G, 4),
+                         "source": "rocprofv3 SQ_INSTS_VALU pass, one pipeline (profiles/pmc_latest.json) "
+                                   "/ avg_launch_ms"}
+    cyc = (load_sq(workload_key, "_cycles_p1") or {}).get(f"{kname}.main")
+    if cyc:
+        roof["wave_cycles"] = {k: round(cyc[k], 4) for k in ("wait_share", "issue_stall_share", "active_share",
+                                                              "lanes_per_valu") if k in cyc}
+        roof["wave_cycles"]["source"] = "rocprofv3 SQ wave-cycle pass, one pipeline (profiles/pmc_latest.json)"
+    return roof
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -400,10 +496,16 @@ def main():
 
     import pathtracerap_amd as P
 
-    # one rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on a 1-GPU
-    # box) ranks share devices round-robin
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-    if world > 1:
+    # one rank per GPU (RCCL); only a gloo rehearsal may put several ranks on one
+    # GPU (round-robin).  device_count() does not initialise HIP on this image.
+    ngpu = torch.cuda.device_count()
+    pg = env_world is not None                # a launcher (or spawn_ranks): a process group, even at world 1
+    if pg:
+        err = check_backend(args.dist_backend, world, ngpu)
+        if err:
+            raise SystemExit(err)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, ngpu)
+    if pg:
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -411,7 +513,7 @@ def main():
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    ctx = Ctx(torch, dist, dev, rank, world)
+    ctx = Ctx(torch, dist, dev, rank, world, pg)
 
     from pathtracerap_amd import synthetic
 
@@ -500,55 +602,27 @@ def main():
         spp = 0 if args.no_full_runs else SPP[name]
         rt = timed_run(P, ctx, st, ct, tk, min(W, 2), 3_000_000, reduce_image=True, full_spp=spp)
         tnpix = ct.width * ct.height
+        troof = None
+        if not args.no_profile and rank == 0 and args.accel != "grid":
+            tkey = target_key(args.accel, name, ct)
+            st1 = one_pipeline_pass(P, torch, dev, st, ct, tk, min(W, 2))
+            troof = trace_roofline(st1, rt["per_bounce"], tk, rt["elapsed"], round(rt["elapsed"] / tk * 1e3, 3),
+                                   "k_trace_bvh" if args.accel == "bvh" else "k_trace_gf", tkey)
+        ctx.barrier()
         targets[name] = {"workload": label, "triangles": st.counts()["nt"], "width": ct.width,
                          "height": ct.height, "bounces": ct.max_bounces, "steps": tk,
                          **rates(rt, tk, tnpix, world), "segments": int(rt["seg"]), "image_finite": rt["img_ok"],
                          "trace_faults": rt["faults"], "host_scene_build_s": round(t_build, 2),
-                         "full_run": full_rates(rt, tnpix)}
+                         "full_run": full_rates(rt, tnpix), "roofline": troof}
         del st
 
     if rank == 0:
         r_main = rates(main_res, K, npix, world)
-        roof = None
         kname = "k_trace_bvh" if args.accel == "bvh" else "k_trace_gf"
-        tb_step = trace_bytes_per_step(per_bounce, K)
-        phases = max(1, len(per_bounce) - 1)                 # trace phases per step
-        b_launch = tb_step / phases                          # algorithmic bytes per launch (one bounce's trace)
-        job = tb_step / (main_res["elapsed"] / K) / 1e9      # per GPU: each rank runs K steps
-        per_step = {"achieved": round(job, 2), "frac": round(job / HBM_PEAK_GBS, 5),
-                    "algorithmic_bytes_per_step": round(tb_step), "ms_per_step": r_main["ms_per_step"],
-                    "note": "whole-job rate: algorithmic trace bytes per step / ms_per_step (16 iterations in "
-                            "flight share the step's wall time)"}
-        if stats1 and stats1.get("trace_launches", 0) > 0 and args.accel != "grid":
-            # Dominant kernel: the persistent trace of bounces >= 1 (k_trace_gf / k_trace_bvh).
-            # Algorithmic bytes per segment entering bounce b >= 1: 32 B ray read (o, d) + 20 B
-            # hit record write; one "launch" = one bounce's trace phase, timed by a HIP event
-            # pair on the stream it is launched on, with one pipeline (no overlap).
-            l1 = stats1["trace_launches"]
-            k1 = stats1["trace_ms"] / l1
-            a1 = b_launch / (k1 / 1e3) / 1e9
-            tr = load_pmc(kname, workload_key)               # PMC HBM bytes per launch, one pipeline
-            roof = {"bound": "hbm", "achieved": round(a1, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(a1 / HBM_PEAK_GBS, 5), "traffic": None if tr is None else round(tr),
-                    "kernel": kname,
-                    "basis": "per launch: algorithmic bytes of one bounce's trace (52 B x segments entering "
-                             "the bounce) / its average duration, HIP events on the launch stream, one "
-                             "pipeline (rocprofv3: profiles/r04/kernel_stats_*_1p.csv); traffic = PMC HBM bytes "
-                             "per launch of the same command (profiles/pmc_latest.json)",
-                    "algorithmic_bytes_per_launch": round(b_launch), "avg_launch_ms": round(k1, 4),
-                    "launches": l1, "trace_phases_per_step": phases, "per_step": per_step,
-                    "sort_avg_ms": round(stats1["sort_ms"] / max(stats1["sort_launches"], 1), 4),
-                    "shade_avg_ms": round(stats1["bounce_ms"] / max(stats1["bounce_launches"], 1), 4),
-                    "scan_avg_ms": round(stats1["scan_ms"] / max(stats1["scan_launches"], 1), 4)}
-            sq1 = load_sq(workload_key, "_sq_p1")
-            kv = (sq1 or {}).get("kernels", {}).get(kname)
-            if kv:
-                g = kv["valu_insts_per_launch"] / (k1 / 1e3) / 1e9
-                roof["issue"] = {"bound": "valu", "unit": "G wave-instr/s", "peak": VALU_PEAK_G,
-                                 "valu_insts_per_launch": round(kv["valu_insts_per_launch"]),
-                                 "achieved": round(g, 1), "frac": round(g / VALU_PEAK_G, 4),
-                                 "source": "rocprofv3 SQ_INSTS_VALU pass, one pipeline (profiles/pmc_latest.json) "
-                                           "/ avg_launch_ms"}
+        roof = None
+        if args.accel != "grid":
+            roof = trace_roofline(stats1, per_bounce, K, main_res["elapsed"], r_main["ms_per_step"], kname,
+                                  workload_key)
         # Issue roofline of the whole job: the traces are bound by instruction issue and
         # dependent-load latency, not by HBM bytes, so the VALU issue rate (all kernels of
         # a step, the pipelines overlapping) against the SIMDs' peak is reported beside it.
@@ -562,7 +636,9 @@ def main():
                              "frac": round(g / VALU_PEAK_G, 4),
                              "salu_insts_per_step": round(sq["salu_insts_per_iteration"]),
                              "salu_achieved": round(sq["salu_insts_per_iteration"] * K / main_res["elapsed"] / 1e9, 1)},
-                     "source": "rocprofv3 SQ_INSTS_VALU / SQ_INSTS_SALU pass (profiles/pmc_latest.json)"}
+                     "iterations_counted": sq.get("iterations"),
+                     "source": "rocprofv3 SQ_INSTS_VALU / SQ_INSTS_SALU pass at the bench's pipelines "
+                               "(profiles/pmc_latest.json); per step = counts / first-bounce dispatches counted"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -580,7 +656,9 @@ def main():
                        "spp_per_step": 1, "accel": args.accel,
                        "results": "bit-identical to the reference algorithm (oracle-checked at this size: "
                                   "tests/test_gpu_configs.py)" if args.accel != "bvh" else "exact closest hit",
-                       "parallelism": f"samples sharded x{world}" + (" (gloo rehearsal)" if world > 1 and args.dist_backend == "gloo" else ""),
+                       "parallelism": f"samples sharded x{world}" + (
+                           "" if not pg else " (gloo rehearsal)" if args.dist_backend == "gloo"
+                           else " (RCCL all-reduce of the float3 accumulator)"),
                        "pipelines": main_res["pipes"], "hw_queues": P.hw_queues(),
                        "segments": int(main_res["seg"]), "primary_segments_cached": int(main_res["seg_primary"]),
                        "segments_per_bounce_rank0": per_bounce,
@@ -589,8 +667,11 @@ def main():
             "roofline": roof, "issue_roofline": issue, "cpu_baseline": cpu, "alt_mode": alt,
             "targets": targets or None,
         }
+        nulled = bound_fracs(out)
+        if nulled:
+            print(f"bench: fraction(s) above 1 not published: {nulled}", file=sys.stderr)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -3,7 +3,10 @@
 A ray's RNG seed depends on its slot in the globally compacted ray pool of
 its iteration, so pixels cannot be split without changing the samples; whole
 iterations can.  Each rank renders a contiguous iteration range into its
-own float3 accumulator and one all-reduce (sum) combines them.
+own float3 accumulator and one all-reduce (sum) combines them.  The
+all-reduce runs whenever a process group exists, at world size 1 too, so a
+one-rank RCCL group exercises the same ordering (the collective on the torch
+stream after the renderer's launches) as the 8-GPU run.
 """
 from __future__ import annotations
 
@@ -31,8 +34,9 @@ def render_sharded(scene, cfg, total_iters: int, device=None,
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
+    grouped = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size() if grouped else 1
+    rank = dist.get_rank() if grouped else 0
     first, n = shard_iterations(total_iters, rank, world)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if render_fn is None else torch.device("cpu")
@@ -46,8 +50,8 @@ def render_sharded(scene, cfg, total_iters: int, device=None,
         r.bind_image(image.data_ptr(), keepalive=image)
         r.allocateOnGPU(scene)
         r.renderLoop(first_iter=first, n_iters=n, sync=False)
-    if world > 1:
-        dist.all_reduce(image, op=dist.ReduceOp.SUM)
+    if grouped:
+        dist.all_reduce(image, op=dist.ReduceOp.SUM)      # RCCL (nccl backend) over xGMI, or gloo
     if render_fn is None:
         torch.cuda.synchronize(device)
         r.free()

@@ -167,3 +167,67 @@ def test_bench_gpus_2_spawns_two_ranks(gpu):
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["trace_faults"] == 0
     assert d["config"]["parallelism"].startswith("samples sharded x2")
+
+
+RCCL_WORKER = r"""
+import os, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+import torch
+import torch.distributed as dist
+import pathtracerap_amd as P
+from pathtracerap_amd.dist import render_sharded
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+s = P.Scene({scene_path!r})
+s.build()
+cfg = P.RenderConfig(width=96, height=72, iterations={iters}, max_bounces=8)
+img = render_sharded(s, cfg, {iters})          # the all-reduce runs through RCCL even at world size 1
+assert img.is_cuda
+np.save({out!r}, img.cpu().numpy())
+dist.destroy_process_group()
+print("rccl ok")
+"""
+
+
+def test_rccl_one_rank_render_sharded_equals_oracle(gpu, pt_mod, oracle_mod, tmp_path):
+    """RCCL loads, initialises (nccl backend, device_id=cuda:0) and orders its
+    all-reduce after the renderer's launches on the torch stream: a one-rank
+    group renders through render_sharded with the collective on the renderer's
+    accumulator, and the image equals the oracle's bit for bit (a one-rank sum
+    is exact)."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    iters = 3
+    scene_path = synthetic.diffuse_scene(str(tmp_path / "scene"), ntri=3000, seed=37, metallic=True)
+    out = str(tmp_path / "img.npy")
+    script = tmp_path / "worker_rccl.py"
+    script.write_text(RCCL_WORKER.format(root=ROOT, scene_path=scene_path, iters=iters, out=out))
+    _run_ranks(script, n=1, timeout=240)
+    got = np.load(out)
+    s = P.Scene(scene_path)
+    s.build()
+    cfg = P.RenderConfig(width=96, height=72, iterations=iters, max_bounces=8)
+    want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg, threads=16))
+    assert np.abs(got).sum() > 0
+    assert np.array_equal(got.view(np.uint32), want.reshape(-1).view(np.uint32))
+
+
+def test_bench_under_a_launcher_with_rccl_one_rank(gpu):
+    """bench.py as the driver's N>1 launch runs it (WORLD_SIZE set, nccl), at one
+    rank: the process group is RCCL, the accumulator all-reduce is inside the
+    timed region, and the line reports it."""
+    import json
+    port = _free_port()
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dist-backend", "nccl",
+                        "--steps", "2", "--warmup", "1", "--targets=", "--alt-accel=", "--no-cpu-baseline",
+                        "--no-full-runs", "--no-profile"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, p.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["trace_faults"] == 0
+    assert "RCCL" in d["config"]["parallelism"]
