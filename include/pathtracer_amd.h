@@ -149,6 +149,12 @@ int pt_renderer_kernel_stats_ex(pt_renderer *r, double *stats, int n);
 int pt_renderer_primary_hits(pt_renderer *r, float *dist, float *normal, int *model);
 int pt_renderer_intersect_rays(pt_renderer *r, int n, const float *orig, const float *dir,
                                float *dist, float *normal, int *model);
+/* Test hook (grid_fast): k_trace_gf's walk certificates (walk_certify_fast,
+ * walk_certify) against the exact stepped walk on the same hit sets of each ray;
+ * out4[4i..4i+3] = fast certificates tried, accepted, accepted-but-wrong,
+ * full certificates accepted-but-wrong (no counterpart in the reference: it
+ * checks the exactness of Renderer.cpp:238-360's replacement). */
+int pt_renderer_certify_check(pt_renderer *r, int n, const float *orig, const float *dir, int *out4);
 void pt_renderer_free(pt_renderer *r);
 
 /* Device math conformance hook: evaluates the kernels' sinf/cosf/powf/sqrtf/div

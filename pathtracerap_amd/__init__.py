@@ -105,6 +105,7 @@ EXPORTS = [
     ("pt_renderer_kernel_stats_ex", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("pt_renderer_primary_hits", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_F, _P_I]),
     ("pt_renderer_intersect_rays", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _P_F, _P_F, _P_F, _P_F, _P_I]),
+    ("pt_renderer_certify_check", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _P_F, _P_F, _P_I]),
     ("pt_renderer_free", None, [ctypes.c_void_p]),
     ("pt_selftest_math", ctypes.c_int, [ctypes.c_int, _P_F, _P_F, _P_F]),
     ("pt_render", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_Cfg), ctypes.c_char_p]),
@@ -383,6 +384,16 @@ class Renderer:
         t = np.zeros(n, np.float32); nn = np.zeros((n, 3), np.float32); m = np.zeros(n, np.int32)
         _err(lib().pt_renderer_intersect_rays(self._h, n, _fp(o), _fp(dd), _fp(t), _fp(nn), _ip(m)), "intersect_rays")
         return t, nn, m
+
+    def certify_check(self, orig, dirs):
+        """grid_fast test hook: per ray, (fast certificates tried, accepted,
+        accepted but disagreeing with the exact walk, full certificates
+        disagreeing) -- an (n, 4) int32 array; both disagreement columns must be 0."""
+        o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+        dd = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        out = np.zeros((len(o), 4), np.int32)
+        _err(lib().pt_renderer_certify_check(self._h, len(o), _fp(o), _fp(dd), _ip(out)), "certify_check")
+        return out
 
     def free(self) -> None:
         if self._h:

@@ -29,7 +29,7 @@ int leaf_max() {
     return v;
 }
 constexpr int kBins = 16;
-constexpr int kMaxDepth = 23;   // <= the kernels' LDS stack (PT_STACK = 24 entries)
+constexpr int kMaxDepth = kMaxBvhDepth;   // pt_types.h: the kernels' LDS stacks are sized (and asserted) for it
 
 struct Box {
     double lo[3] = {1e300, 1e300, 1e300};

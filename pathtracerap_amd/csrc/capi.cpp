@@ -289,6 +289,10 @@ int pt_renderer_intersect_rays(pt_renderer* r, int n, const float* o, const floa
     if (n < 0 || (n > 0 && (!o || !d || !t || !nn || !m))) return set_err("bad arguments");
     R_CALL(r->r->intersectRays(n, o, d, t, nn, m));
 }
+int pt_renderer_certify_check(pt_renderer* r, int n, const float* o, const float* d, int* out4) {
+    if (n < 0 || (n > 0 && (!o || !d || !out4))) return set_err("bad arguments");
+    R_CALL(r->r->certifyCheck(n, o, d, out4));
+}
 void pt_renderer_free(pt_renderer* r) {
     if (!r) return;
     delete r->r;

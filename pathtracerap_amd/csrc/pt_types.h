@@ -23,6 +23,12 @@ enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2,
 //              ACCEL_GRID; needs the BVH.
 enum Accel : int { ACCEL_GRID = 0, ACCEL_BVH = 1, ACCEL_GRID_FAST = 2 };
 
+// Deepest BLAS inner-node level below a root (bvh.cpp's builder caps the depth
+// here).  A traversal holds at most one deferred sibling per level, so a lane's
+// stack needs kMaxBvhDepth entries; renderer.hip asserts its LDS stacks (kStack)
+// hold that many, since k_trace_bvh and the one-lane paths have no spill path.
+constexpr int kMaxBvhDepth = 23;
+
 // One instance (Model, Primitive.h:94-101) flattened for the traces: 62
 // dwords (the material, which only the shading pass reads, is ModelShade), so
 // k_trace_gf stages up to 12 of them in LDS at 16 resident waves per CU.

@@ -134,6 +134,8 @@ public:
     int segmentsPerBounce(long long* out, int n);
     int primaryHits(float* dist, float* normal, int* model);
     int intersectRays(int n, const float* orig, const float* dir, float* dist, float* normal, int* model);
+    // test hook (grid_fast): walk certificates vs the exact walk on the same hit sets; 4 ints per ray
+    int certifyCheck(int n, const float* orig, const float* dir, int* out4);
 
     RenderConfig cfg;
     std::string last_error;

@@ -60,7 +60,10 @@ constexpr int kBlock = 256;
 #define PT_NODE_STEP 8        // k_trace_gf: node visits per node step (lanes still at an inner node go on)
 #endif
 constexpr int kAccelHitBuffer = 3;   // k_bounce template value: hits come from k_trace_bvh
-constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS), >= kMaxDepth + 2
+constexpr int kStack = PT_STACK;   // BVH traversal stack entries per lane (LDS)
+// k_trace_bvh, k_trace_deferred and the one-lane paths push at most one sibling per
+// BLAS level and have no spill path: a smaller stack would overwrite other lanes' LDS
+static_assert(kStack >= kMaxBvhDepth + 1, "PT_STACK must hold a full BLAS path (pt_types.h kMaxBvhDepth + 1)");
 constexpr int kSortBits = 12, kSortBins = 1 << kSortBits;   // ray sort key (k_sort_hist / k_sort_scatter)
 #ifndef PT_SORT_WG
 #define PT_SORT_WG 512
@@ -1676,6 +1679,71 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
+
+// Test hook: the walk certificates against the exact walk on the same hit set.
+// k_trace_gf's main launch decides most walks by walk_certify_fast (and, where it
+// declines, walk_certify) without stepping the DDA; this kernel runs both on the
+// hit set of every model an arbitrary world-space ray enters (grid_hitset's entry
+// test), collected as the bounded first tier (window wdelta) and as the unbounded
+// last tier, with the members in registers exactly as k_trace_gf holds them, and
+// compares every certificate that accepts with hitset_walk_g's stepped result
+// (no certificate, STRICT as in k_trace_gf): hit, minimum t, triangle and
+// finality must all agree.  out[i] = (fast tried, fast accepted, fast accepted but
+// wrong, full accepted but wrong), summed over the ray's models and both tiers.
+__global__ __launch_bounds__(kBlock) void k_certify_check(KParams p, int n, const float* orig, const float* dir,
+                                                         int4* out) {
+    __shared__ int s_stack[kStack * kBlock];
+    __shared__ int4 s_hs[kHitCap * kBlock];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    int* stack = s_stack + threadIdx.x;
+    int4* hs = s_hs + threadIdx.x;
+    const f3 ow = mk3(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
+    const f3 dw = mk3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    int tried = 0, fast_ok = 0, fast_bad = 0, full_bad = 0;
+    for (int im = 0; im < p.nmodels; im++) {
+        const ModelRec& M = p.models[im];
+        const f3 o = xform12(M.w2m, ow, 1.0f);
+        const f3 d = normalize(xform12(M.w2m, dw, 0.0f));
+        const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
+        float t_box;
+        if (!slab_ref(M.bbox, o, d, inv, t_box)) continue;
+        const f3 pt = o + d * t_box;
+        if ((pt.x - M.bbox[0]) < -kEps || (pt.y - M.bbox[1]) < -kEps || (pt.z - M.bbox[2]) < -kEps) continue;
+        const f3 ninv = node_inv(inv);
+        const bool exact_inv = (absr(ninv.x) < 1e30f) & (absr(ninv.y) < 1e30f) & (absr(ninv.z) < 1e30f);
+        for (int tier = 0; tier < 2; tier++) {
+            const float win = tier == 0 ? M.wdelta : 3.0e38f;
+            float tmin;
+            const int nh = tier == 0 ? bvh_collect<kBlock, true>(p, M, o, d, ninv, stack, hs, &tmin, win + M.reach)
+                                     : bvh_collect<kBlock, false>(p, M, o, d, ninv, stack, hs, &tmin, 3.0e38f);
+            if (nh <= 0 || nh > kGfHitCap) continue;     // k_trace_gf certifies LDS-held sets only
+            int4 mem[kGfHitCap];
+#pragma unroll
+            for (int h = 0; h < kGfHitCap; h++) mem[h] = h < nh ? hs[h * kBlock] : make_int4(0, 0, 0, 0);
+            auto get = [&](int h) { return mem[h]; };
+            const WalkResult w = hitset_walk_g<kGfHitCap, decltype(get), false, true>(p, M, d, inv, pt, t_box,
+                                                                                         get, nh, tmin, win);
+            auto agrees = [&](int tri) {
+                const bool final_ = tier == 1 || w.final_min || w.tw < tmin + win;
+                return w.hit && w.has_best && w.t == tmin && w.tri == tri && final_;
+            };
+            int tri = -1;
+            if (exact_inv) {
+                tried++;
+                if (walk_certify_fast<kGfHitCap>(p, M, d, ninv, pt, t_box, get, nh, tmin, win, tri)) {
+                    fast_ok++;
+                    if (!agrees(tri)) fast_bad++;
+                }
+            }
+            tri = -1;
+            if (walk_certify<kGfHitCap>(p, M, d, inv, pt, t_box, get, nh, tmin, win, tri) && !agrees(tri))
+                full_bad++;
+        }
+    }
+    out[i] = make_int4(tried, fast_ok, fast_bad, full_bad);
+}
+
 // Collection window of k_trace_gf, on voxel boxes instead of the reach R: the
 // walk can enter member h's voxel box before X = t_min + window only if the
 // exact ray enters that box grown by ModelRec::cslack (the DDA's deviation from
@@ -1867,16 +1935,17 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         // safety net: never spin forever (reported as a fault); checked every 16th iteration, so
         // the cap's kernel-argument load stays out of the loop's common path
         if ((iters & 15u) == 0 && iters > p.trace_iter_cap) {
-            // the faulting wave's lanes (slots 34..38: idle, done, select, node/leaf/walk; exhausted waves)
+            // the faulting wave's lanes (slots 59..63: idle, done, select, node/leaf/walk; exhausted
+            // waves) -- slots no PT_DEBUG_ABLATE statistic uses
             const int f0 = __popcll(__ballot(state == 0)), f3 = __popcll(__ballot(state == 3)),
                       f1 = __popcll(__ballot(state == 1));
             if (lane == 0) {
                 atomicAdd(p.segments + kTraceFaultCounter, 1ull);
-                atomicAdd(p.segments + 34 + kMaxBounceCounters, (unsigned long long)f0);
-                atomicAdd(p.segments + 35 + kMaxBounceCounters, (unsigned long long)f3);
-                atomicAdd(p.segments + 36 + kMaxBounceCounters, (unsigned long long)f1);
-                atomicAdd(p.segments + 37 + kMaxBounceCounters, (unsigned long long)(64 - f0 - f3 - f1));
-                atomicAdd(p.segments + 38 + kMaxBounceCounters, exhausted ? 1ull : 0ull);
+                atomicAdd(p.segments + 59 + kMaxBounceCounters, (unsigned long long)f0);
+                atomicAdd(p.segments + 60 + kMaxBounceCounters, (unsigned long long)f3);
+                atomicAdd(p.segments + 61 + kMaxBounceCounters, (unsigned long long)f1);
+                atomicAdd(p.segments + 62 + kMaxBounceCounters, (unsigned long long)(64 - f0 - f3 - f1));
+                atomicAdd(p.segments + 63 + kMaxBounceCounters, exhausted ? 1ull : 0ull);
             }
             break;
         }
@@ -2712,6 +2781,12 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     {
         const char* dbg = std::getenv("PT_DEBUG_ABLATE");   // timing-only ablations; results become wrong
         kp.debug = dbg ? std::atoi(dbg) : 0;
+        // bits 4 (walk / certificate statistics, slots 20..28 and 32..39) and 32 (cycle stamps,
+        // slots 20..27) count into the same diagnostic slots: one at a time
+        if ((kp.debug & 4) && (kp.debug & 32)) {
+            last_error = "PT_DEBUG_ABLATE: bits 4 and 32 share diagnostic slots; set one at a time";
+            return -1;
+        }
         // persistent-trace safety net; tests lower it to exercise the fault report
         const char* cap = std::getenv("PT_TRACE_ITER_CAP");
         kp.trace_iter_cap = cap ? (unsigned)std::strtoul(cap, nullptr, 10) : (1u << 26);
@@ -2738,7 +2813,11 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         if (cfg.accel == ACCEL_GRID_FAST) split_trace = eg ? std::atoi(eg) != 0 : true;
         // trace variants: 9 / 11 model records in LDS (the default), 8 / 10 from global memory
         const char* gff = std::getenv("PT_GF_FLAGS");
-        gf_flags = gff ? std::atoi(gff) : 9;
+        // each flag is checked only where it applies (split grid_fast / split bvh): a leftover
+        // value does not fail a render whose trace never reads it
+        const bool gf_split = split_trace && cfg.accel == ACCEL_GRID_FAST;
+        const bool bvh_split = split_trace && cfg.accel == ACCEL_BVH;
+        gf_flags = gff && gf_split ? std::atoi(gff) : 9;
         if (gf_flags != 8 && gf_flags != 9) { last_error = "PT_GF_FLAGS must be 8 or 9"; return -1; }
         // 9..12 instances: the default variants with room for 12 LDS model records (F | 32)
         gf_wide_lds = (gf_flags & ~1) == 8 && (gf_flags & 1) && scene.model_recs.size() > (size_t)kLdsModelsGf &&
@@ -2747,7 +2826,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
-        kp.trace_flags = tf ? std::atoi(tf) : 11;
+        kp.trace_flags = tf && bvh_split ? std::atoi(tf) : 11;
         if (kp.trace_flags != 10 && kp.trace_flags != 11) { last_error = "PT_TRACE_FLAGS must be 10 or 11"; return -1; }
         // the default variant with 9..12 models: model records in LDS with room for 12 (F | 32)
         bvh_wide_lds = kp.trace_flags == 11 && scene.model_recs.size() > (size_t)kLdsModels &&
@@ -3283,6 +3362,26 @@ int Renderer::intersectRays(int n, const float* orig, const float* dir, float* d
     PT_HIP(hipMemcpyAsync(model, d_m, n * 4, hipMemcpyDeviceToHost, stream));
     PT_HIP(hipStreamSynchronize(stream));
     hipFree(d_o); hipFree(d_d); hipFree(d_t); hipFree(d_n); hipFree(d_m);
+    return 0;
+}
+
+int Renderer::certifyCheck(int n, const float* orig, const float* dir, int* out4) {
+    if (!allocated) { last_error = "not allocated"; return -1; }
+    if (cfg.accel != ACCEL_GRID_FAST) { last_error = "certify_check needs accel grid_fast (the BLAS hit sets)"; return -1; }
+    if (n <= 0) return 0;
+    float *d_o, *d_d;
+    int4* d_out;
+    PT_HIP(hipMalloc(&d_o, n * 12));
+    PT_HIP(hipMalloc(&d_d, n * 12));
+    PT_HIP(hipMalloc(&d_out, n * sizeof(int4)));
+    PT_HIP(hipMemcpyAsync(d_o, orig, n * 12, hipMemcpyHostToDevice, stream));
+    PT_HIP(hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, stream));
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(k_certify_check, grid, dim3(kBlock), 0, stream, kp, n, d_o, d_d, d_out);
+    PT_HIP(hipGetLastError());
+    PT_HIP(hipMemcpyAsync(out4, d_out, n * sizeof(int4), hipMemcpyDeviceToHost, stream));
+    PT_HIP(hipStreamSynchronize(stream));
+    hipFree(d_o); hipFree(d_d); hipFree(d_out);
     return 0;
 }
 

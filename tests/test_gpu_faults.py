@@ -40,7 +40,7 @@ def test_trace_iteration_cap_is_an_error(gpu, pt_mod, synth_dir, monkeypatch, ac
 
 def test_trace_fault_records_the_stuck_lanes(gpu, pt_mod, synth_dir, monkeypatch):
     """A k_trace_gf wave that gives up records its 64 lanes by state in diagnostic
-    slots 34..37 (idle, done, select, node/leaf/walk) and counts itself in 38 when its
+    slots 59..62 (idle, done, select, node/leaf/walk) and counts itself in 63 when its
     ray pool was exhausted (renderer.hip, the iteration-cap check): scripts/hangcheck.py
     prints them, which is how the state-7 livelock of round 4 was found."""
     P = pt_mod
@@ -54,10 +54,10 @@ def test_trace_fault_records_the_stuck_lanes(gpu, pt_mod, synth_dir, monkeypatch
         r.synchronize()
     faults = r.trace_faults()
     v = r.segments_per_bounce(128)
-    lanes = [v[63 + slot] for slot in range(34, 38)]
+    lanes = [v[63 + slot] for slot in range(59, 63)]
     assert faults > 0
     assert sum(lanes) == 64 * faults, (lanes, faults)
-    assert 0 <= v[63 + 38] <= faults
+    assert 0 <= v[63 + 63] <= faults
     r.free()
 
 
@@ -105,3 +105,27 @@ def test_graph_replay_rebind_image_between_loops(gpu, pt_mod, oracle_mod, synth_
     want_b, _ = O.render(flat, oc)
     assert_bitexact(got_a, want_a, "accumulator bound first")
     assert_bitexact(got_b, want_b, "accumulator bound second")
+
+
+def test_trace_flags_checked_only_where_they_apply(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch):
+    """A leftover PT_GF_FLAGS / PT_TRACE_FLAGS value fails allocateOnGPU only for
+    the trace that reads it: the reference grid mode renders as usual (and equals
+    the oracle), while grid_fast refuses an invalid PT_GF_FLAGS and bvh an
+    invalid PT_TRACE_FLAGS."""
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_GF_FLAGS", "13")
+    monkeypatch.setenv("PT_TRACE_FLAGS", "27")
+    s = _scene(P, synth_dir)
+    cfg = P.RenderConfig(width=40, height=32, iterations=1, max_bounces=4, accel=P.ACCEL_GRID)
+    r = P.Renderer(cfg)
+    r.allocateOnGPU(s)
+    r.renderLoop()
+    img = r.image()
+    r.free()
+    want, _ = O.render(flat_from_export(s.export()), oracle_cfg(cfg))
+    assert_bitexact(img, want, "grid mode with leftover trace flags")
+    for accel, flag in ((P.ACCEL_GRID_FAST, "PT_GF_FLAGS"), (P.ACCEL_BVH, "PT_TRACE_FLAGS")):
+        r = P.Renderer(P.RenderConfig(width=40, height=32, iterations=1, max_bounces=4, accel=accel))
+        with pytest.raises(P.PathTracerError, match=flag):
+            r.allocateOnGPU(s)
+        r.free()

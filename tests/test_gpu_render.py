@@ -353,6 +353,52 @@ def test_grid_fast_voxel_boundary_rays(gpu, pt_mod, oracle_mod):
     assert_bitexact(tt, ot, "dist")
 
 
+def _boundary_scene(P):
+    from pathtracerap_amd.synthetic import room_mesh, torus_mesh
+    s = P.Scene()
+    t = s.addMesh(*torus_mesh(3000, seed=2))
+    rm = s.addMesh(*room_mesh())
+    s.addModel(t, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.addModel(rm, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (0.5, 0.5, 0.5))
+    s.build(bvh=True)
+    return s
+
+
+def _interior_rays(n, seed):
+    """Bounce-like rays: origins anywhere in the room, directions uniform on the
+    sphere, a third of them nearly axis-parallel (one or two slopes 1e-7..1e-3)."""
+    rs = np.random.RandomState(seed)
+    o = rs.uniform([-4.9, 0.05, -4.9], [4.9, 9.9, 4.9], (n, 3))
+    d = rs.normal(size=(n, 3))
+    m = rs.rand(n) < 0.33
+    for _ in range(2):
+        ax = rs.randint(0, 3, n)
+        d[m, ax[m]] *= 10.0 ** rs.uniform(-7, -3, m.sum())
+        m &= rs.rand(n) < 0.5
+    return o.astype(np.float32), d.astype(np.float32)
+
+
+def test_walk_certificates_agree_with_the_exact_walk(gpu, pt_mod):
+    """k_trace_gf's main launch decides most walks by walk_certify_fast (and
+    walk_certify where it declines) instead of stepping the DDA.  On boundary
+    rays (origins and targets on voxel boundaries, near-axis-parallel slopes)
+    and bounce-like interior rays, every certificate that accepts must equal
+    the exact walk's (hit, t, triangle, finality) on the same hit set -- the
+    first tier's window and the unbounded tier, members in registers as in
+    k_trace_gf (renderer.hip k_certify_check)."""
+    P = pt_mod
+    s = _boundary_scene(P)
+    a = s.export()
+    r = P.Renderer(P.RenderConfig(width=8, height=8, accel=P.ACCEL_GRID_FAST))
+    r.allocateOnGPU(s)
+    for o, d in (_boundary_rays(a, 60000, 11), _interior_rays(60000, 12)):
+        c = r.certify_check(o, d)
+        tried, ok, fast_bad, full_bad = c.sum(0)
+        assert fast_bad == 0 and full_bad == 0, (tried, ok, fast_bad, full_bad)
+        assert tried > 20000 and ok > 0.5 * tried, (tried, ok)
+    r.free()
+
+
 @pytest.mark.parametrize("accel", [1, 2])
 def test_pipelines_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, accel):
     """1..16 iterations in flight (own streams, contribution buffers merged in
