@@ -56,6 +56,12 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 VALU_PEAK_G = 256 * 4 * 2.4 / 2
 # samples per pixel each BASELINE.json configuration asks for (full_run)
 SPP = {"configs1": 256, "target_1m": 1024, "configs2": 1024, "configs4": 4096}
+# What "bit-exact" means here: the reference is CUDA + thrust + Assimp + MSVC and
+# cannot be built in this image, so parity is against its C restatement, which is
+# pinned to the reference's own output image (tests/golden/oracle_pin_stats.json)
+PARITY_BASIS = ("bit-exact vs the C restatement of the reference algorithm (oracle/ptoracle.c; checked at this "
+                "size by tests/test_gpu_configs.py); the restatement is within 1 LSB of the reference's Render.bmp "
+                "on 99.4 % of channels (max 4), not bit-exact vs the CUDA binary, which cannot be built here")
 
 
 def parse(argv=None):
@@ -654,8 +660,7 @@ def main():
             "config": {"workload": workload_name(args),
                        "triangles": ntri, "width": cfg.width, "height": cfg.height, "bounces": cfg.max_bounces,
                        "spp_per_step": 1, "accel": args.accel,
-                       "results": "bit-identical to the reference algorithm (oracle-checked at this size: "
-                                  "tests/test_gpu_configs.py)" if args.accel != "bvh" else "exact closest hit",
+                       "results": PARITY_BASIS if args.accel != "bvh" else "exact closest hit",
                        "parallelism": f"samples sharded x{world}" + (
                            "" if not pg else " (gloo rehearsal)" if args.dist_backend == "gloo"
                            else " (RCCL all-reduce of the float3 accumulator)"),

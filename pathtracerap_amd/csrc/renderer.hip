@@ -1631,6 +1631,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     }
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        if (TAIL) {                                 // the tail launches' share (slots 15, 43)
+            atomicAdd(p.segments + 15 + kMaxBounceCounters, st_iter);
+            atomicAdd(p.segments + 43 + kMaxBounceCounters, st_busy);
+        }
         atomicAdd(p.segments + 44 + kMaxBounceCounters, st_drain);
         atomicAdd(p.segments + 45 + kMaxBounceCounters, st_drain_busy);
         atomicAdd(p.segments + 46 + kMaxBounceCounters, st_busy);
@@ -2303,6 +2307,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     }
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
+        if (TAIL) {                                 // the tail launches' share (slots 15, 43)
+            atomicAdd(p.segments + 15 + kMaxBounceCounters, st_iter);
+            atomicAdd(p.segments + 43 + kMaxBounceCounters, st_busy);
+        }
         atomicAdd(p.segments + 44 + kMaxBounceCounters, st_drain);
         atomicAdd(p.segments + 45 + kMaxBounceCounters, st_drain_busy);
         atomicAdd(p.segments + 46 + kMaxBounceCounters, st_busy);
@@ -2495,6 +2503,13 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
         atomicAdd(p.segments, (unsigned long long)n);           // shared by concurrent pipelines
         if (bounce < kMaxBounceCounters) atomicAdd(p.segments + 1 + bounce, (unsigned long long)n);
         p.dst_start[(total + CH - 1) / CH] = nb > 0 ? nb - 1 : 0;
+        if (PT_TRACE_STATS && bounce > 0) {    // hand-on volume of the bounce's trace (slots 47..50)
+            atomicAdd(p.segments + 47 + kMaxBounceCounters, (unsigned long long)p.cont_count[0]);   // drained at level 0
+            atomicAdd(p.segments + 48 + kMaxBounceCounters,                                        // walk hand-ons
+                      (unsigned long long)min(p.cont_count[kDrainLevels], p.cont_wcap));
+            atomicAdd(p.segments + 49 + kMaxBounceCounters, (unsigned long long)*p.defer_count);    // deferred rays
+            atomicAdd(p.segments + 50 + kMaxBounceCounters, (unsigned long long)p.cont_count[1]);   // drained at level 1
+        }
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
         *p.defer_count = 0;        // and no deferred grid_fast rays

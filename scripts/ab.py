@@ -91,6 +91,12 @@ def main():
             out[v]["drain_iter_share"] = round(allc[107] / it, 3)
             out[v]["busy_lanes_per_drain_iter"] = round(allc[108] / max(allc[107], 1), 2)
             out[v]["phase_iters_per_segment"] = {k: round(a / sg, 3) for k, (a, b) in ph.items()}
+            out[v]["tail_iter_share"] = round(allc[78] / it, 3)          # slot 15: tail launches' wave-iterations
+            out[v]["busy_lanes_per_tail_iter"] = round(allc[106] / max(allc[78], 1), 2)   # slot 43
+        if any(allc[110:114]):                         # slots 47..50 (k_scan, stats build): hand-on volume
+            sg = max(rs[v].segments(), 1)
+            out[v]["handons_per_segment"] = dict(zip(["drained_l0", "walk_handons", "deferred", "drained_l1"],
+                                                     [round(c / sg, 5) for c in allc[110:114]]))
         if "PT_DEBUG_ABLATE=32" in v or "PT_DEBUG_ABLATE=96" in v:   # cycle stamps
             cyc = allc[83:89]
             tot = max(sum(cyc), 1)
