@@ -109,6 +109,11 @@ int pt_scene_export(const pt_scene *s, float *vpos, float *vnrm, int *tris, int 
 /* BVH export (ACCEL_BVH builds): nodes nbvh_nodes*16 (the 64-byte BvhNode as
  * 16 floats; int fields bit-cast), refs nbvh_refs, roots nmesh. */
 int pt_scene_export_bvh(const pt_scene *s, float *nodes, int *refs, int *roots);
+/* The same BLAS collapsed 4-wide (k_trace_gf's node steps): Bvh4Node records,
+ * 32 words each (lo x/y/z[4], hi x/y/z[4], link[4], count[4]), and each mesh's
+ * 4-wide root (-1: none).  Returns the node count (call with nodes = NULL to
+ * size the buffer), < 0 on error. */
+int pt_scene_export_bvh4(const pt_scene *s, float *nodes, int *roots);
 
 /* ---- Renderer ---- */
 pt_renderer *pt_renderer_create(const pt_render_config *cfg);

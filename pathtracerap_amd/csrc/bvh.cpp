@@ -274,4 +274,77 @@ int Scene::relayoutPairs(int n0, int root) {
     return nid[root - n0];
 }
 
+// 4-wide collapse (Bvh4Node): each 4-wide node takes a binary node's children,
+// replacing every inner child by that child's own two children, so it holds
+// 2..4 slots; inner slots become 4-wide nodes in turn (depth-first, a node's
+// inner children next to each other).  Boxes are copied bit for bit.  A mesh
+// whose leaves do not fit the traversal stack's leaf encoding (more than
+// kMaxLeafCount4 triangles, or a first index >= 2^kLeafCountShift) gets no
+// 4-wide BLAS (root -1) and k_trace_gf's binary node steps trace it.
+void Scene::buildBvh4() {
+    bvh4_nodes.clear();
+    mesh_bvh4_root.assign(meshes.size(), -1);
+    if (bvh_nodes.empty()) return;
+    struct Slot { float lo[3], hi[3]; int link, count; };
+    auto child = [&](const BvhNode& nd, int c) {
+        Slot s;
+        for (int k = 0; k < 3; k++) {
+            s.lo[k] = c ? nd.lo1[k] : nd.lo0[k];
+            s.hi[k] = c ? nd.hi1[k] : nd.hi0[k];
+        }
+        s.link = c ? nd.link1 : nd.link0;
+        s.count = c ? nd.count1 : nd.count0;
+        return s;
+    };
+    for (size_t m = 0; m < meshes.size(); m++) {
+        const int root = mesh_bvh_root[m];
+        if (root < 0) continue;
+        const size_t n0 = bvh4_nodes.size();
+        bool fits = true;
+        // make(b): the 4-wide node for binary node b; returns its index
+        std::vector<std::pair<int, int>> work;   // (binary node, 4-wide index) still to fill
+        auto alloc = [&](int b) {
+            const int id = (int)bvh4_nodes.size();
+            bvh4_nodes.push_back(Bvh4Node());
+            work.push_back({b, id});
+            return id;
+        };
+        const int r4 = alloc(root);
+        for (size_t w = 0; w < work.size(); w++) {
+            const int b = work[w].first, id = work[w].second;
+            Slot slots[4];
+            int ns = 0;
+            const BvhNode nd = bvh_nodes[b];
+            for (int c = 0; c < 2; c++) {
+                const Slot s = child(nd, c);
+                if (s.count == 0) {
+                    const BvhNode g = bvh_nodes[s.link];
+                    slots[ns++] = child(g, 0);
+                    slots[ns++] = child(g, 1);
+                } else {
+                    slots[ns++] = s;
+                }
+            }
+            Bvh4Node out;
+            std::memset(&out, 0, sizeof out);
+            for (int c = 0; c < 4; c++) {
+                Slot s;
+                if (c < ns) s = slots[c];
+                else { for (int k = 0; k < 3; k++) { s.lo[k] = 1.0f; s.hi[k] = -1.0f; } s.link = -1; s.count = -1; }
+                if (s.count > 0 && (s.count > kMaxLeafCount4 || s.link >= (1 << kLeafCountShift))) fits = false;
+                out.lox[c] = s.lo[0]; out.loy[c] = s.lo[1]; out.loz[c] = s.lo[2];
+                out.hix[c] = s.hi[0]; out.hiy[c] = s.hi[1]; out.hiz[c] = s.hi[2];
+                out.count[c] = s.count;
+                out.link[c] = s.count == 0 ? alloc(s.link) : s.link;   // binary index -> 4-wide index
+            }
+            bvh4_nodes[id] = out;
+        }
+        if (fits) {
+            mesh_bvh4_root[m] = r4;
+        } else {
+            bvh4_nodes.resize(n0);
+        }
+    }
+}
+
 }  // namespace pt

@@ -193,6 +193,15 @@ int pt_scene_export_bvh(const pt_scene* s, float* nodes, int* refs, int* roots) 
     return 0;
 }
 
+int pt_scene_export_bvh4(const pt_scene* s, float* nodes, int* roots) {
+    if (!s) return set_err("null scene");
+    const pt::Scene& S = s->s;
+    if (nodes && !S.bvh4_nodes.empty()) std::memcpy(nodes, S.bvh4_nodes.data(), S.bvh4_nodes.size() * sizeof(pt::Bvh4Node));
+    if (roots)
+        for (size_t i = 0; i < S.meshes.size(); i++) roots[i] = S.mesh_bvh4_root.empty() ? -1 : S.mesh_bvh4_root[i];
+    return (int)S.bvh4_nodes.size();
+}
+
 pt_renderer* pt_renderer_create(const pt_render_config* c) {
     if (!c) { set_err("null config"); return nullptr; }
     if (c->accel != PT_ACCEL_GRID && c->accel != PT_ACCEL_BVH && c->accel != PT_ACCEL_GRID_FAST) {

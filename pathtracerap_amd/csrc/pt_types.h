@@ -44,7 +44,7 @@ struct ModelRec {
     int bvh_root;         // index of the mesh's BLAS root node
     float wbox[6];        // conservative world-space AABB of everything the instance can hit
     float reach;          // R: max over triangles of the (tolerance-grown) voxel-box diameter, model units
-    int pad0;             // (was the 4-wide BLAS root; keeps the 62-dword record)
+    int bvh4_root;        // index of the mesh's 4-wide BLAS root (Bvh4Node), -1: trace the binary one
     float wdelta;         // tier-1 window: the walk is exact up to t_min + wdelta
     float ivw[3];         // 1 / vw (rounded; walk certificate only, used with margins)
     float cslack[3];      // walk certificate: position slack per axis (DDA +EPSILON shift + rounding)
@@ -67,6 +67,25 @@ struct BvhNode {
     float hi1[3]; int count1;
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
+
+// 4-wide BLAS node for k_trace_gf's node steps: a binary node and its two
+// children collapsed, so one 128-byte fetch (one dependent round trip) tests
+// what the binary layout tests in two.  Child c's box is (lo*[c], hi*[c]);
+// count[c] -1 = empty, 0 = inner (link = Bvh4Node index), > 0 = leaf (link =
+// first bvh_tri_order entry).  The same boxes as the binary nodes: only the
+// number of fetches per traversal changes, never the set of triangles tested.
+struct Bvh4Node {
+    float lox[4], loy[4], loz[4];
+    float hix[4], hiy[4], hiz[4];
+    int link[4];
+    int count[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
+// Leaf children pushed on k_trace_gf's 4-wide traversal stack are encoded as
+// (1 << 31) | (count << kLeafCountShift) | first: count <= kMaxLeafCount4,
+// first < 2^kLeafCountShift (Scene::buildBvh4 checks both).
+constexpr int kLeafCountShift = 26;
+constexpr int kMaxLeafCount4 = 31;
 
 
 }  // namespace pt

@@ -45,6 +45,7 @@ struct KParams {
     const int2* voxels;         // (start, end)
     const int* per_voxel;
     const BvhNode* bvh;
+    const Bvh4Node* bvh4;       // the same BLAS 4-wide (k_trace_gf node steps; nullptr when the scene has none)
     const int* bvh_tri;
     const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
     int* spill;                 // traversal-stack spill beyond the LDS entries, lane-minor
@@ -70,6 +71,8 @@ struct KParams {
     int* hitm;                          // per-slot model
     int* trace_next;                    // persistent trace: next unclaimed source block, reset by k_scan
     int trace_refill;                   // refill a wave's idle lanes once this many are idle
+    int trace_rpl;                      // main trace launch: waves beyond ceil(n / (64 * trace_rpl)) exit at once (0: off)
+    int trace_min_blocks;               // ... but at least this many waves run
     int trace_flags;                    // k_trace_bvh variant: 11 LDS model records, 10 global
     int* defer_slots;                   // k_trace_gf: slots whose hit set overflowed LDS (k_trace_deferred)
     int* defer_count;                   // reset by k_scan
@@ -79,6 +82,7 @@ struct KParams {
     unsigned short* sort_key;           // per source index of the previous bounce's pool
     int sort_mode;                      // key layout (k_sort_hist); 0 = no sort
     float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
+    unsigned sort_heavy;                // sort modes 9 / 10: models whose BLAS makes a ray expensive (bit mask)
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
     int* cont;                          // drain continuations: rays a persistent trace handed on (SoA, stride cont_cap)
     int cont_cap;

@@ -1340,6 +1340,13 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     const bool may_dump = level < p.drain_levels;
     const int ncont = TAIL ? p.cont_count[level - 1] : 0;
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
+    // Sparse bounces: a main launch whose rays come to fewer than trace_rpl per lane runs only
+    // as many waves as give each lane that many (the rest exit at once), so fewer waves pay
+    // the drain -- the wait on each wave's slowest rays once the claim counter runs out.
+    if (!TAIL && p.trace_rpl > 0) {
+        const int n_b = p.n_live[bounce];
+        if ((int)blockIdx.x >= max(p.trace_min_blocks, (n_b + BS * p.trace_rpl - 1) / (BS * p.trace_rpl))) return;
+    }
     // F & 1 is launched only when the scene has at most kLdsModels models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
     // never flat loads through a generic pointer.
@@ -1682,7 +1689,17 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
+#ifndef PT_GF_BVH4
+#define PT_GF_BVH4 1          // k_trace_gf: node steps over the 4-wide BLAS (Bvh4Node); 0: the binary one
+#endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
+constexpr bool kGfBvh4 = PT_GF_BVH4 != 0;
+// 4-wide traversal: at most 3 pushes per node on a path of at most (kMaxBvhDepth + 1) / 2 + 1 nodes
+static_assert(!kGfBvh4 || 3 * ((kMaxBvhDepth + 1) / 2 + 1) + 1 <= kGfStack + kSpillEntries,
+              "k_trace_gf's 4-wide traversal stack (LDS + spill) too small");
+__device__ __forceinline__ int leaf_entry4(int first, int count) {
+    return (int)(0x80000000u | ((unsigned)count << kLeafCountShift) | (unsigned)first);
+}
 
 // Test hook: the walk certificates against the exact walk on the same hit set.
 // k_trace_gf's main launch decides most walks by walk_certify_fast (and, where it
@@ -1809,6 +1826,13 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     const int nd = TAIL ? p.cont_count[level - 1] : 0;
     const int ncont = nd + (TAIL && level == 1 ? min(p.cont_count[kDrainLevels], p.cont_wcap) : 0);
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
+    // Sparse bounces: a main launch whose rays come to fewer than trace_rpl per lane runs only
+    // as many waves as give each lane that many (the rest exit at once), so fewer waves pay
+    // the drain -- the wait on each wave's slowest rays once the claim counter runs out.
+    if (!TAIL && p.trace_rpl > 0) {
+        const int n_b = p.n_live[bounce];
+        if ((int)blockIdx.x >= max(p.trace_min_blocks, (n_b + BS * p.trace_rpl - 1) / (BS * p.trace_rpl))) return;
+    }
     // F & 1 is launched only when the scene has at most kLdsModelsGf models: the
     // choice is compile-time, so model reads are ds_read (LDS) or global loads,
     // never flat loads through a generic pointer.
@@ -2036,7 +2060,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 if (PT_TRACE_STATS && (p.debug & 1024)) G = mk3(0, 0, 0);   // timing-only ablation: no growth
                 tier = 0;
                 win = (PT_TRACE_STATS && (p.debug & 256)) ? 0.0f : M.wdelta;   // 256: timing-only ablation
-                cur = M.bvh_root;
+                cur = kGfBvh4 ? M.bvh4_root : M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax; pblk = -1;
                 state = 2;
                 break;
@@ -2110,7 +2134,21 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     }
                 }
             }
-            if (state == 4) {
+            if (kGfBvh4 && state == 4) {
+                lf_i += n_step;
+                // end of the leaf: the next stack entry, a leaf (encoded, < 0) or a node
+                const bool end = lf_i == lf_e;
+                const bool pop = end & (sp > 0);
+                collected = end & (sp == 0);
+                const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
+                sp -= pop ? 1 : 0;
+                const bool tleaf = pop & (top < 0);
+                const int first = top & ((1 << kLeafCountShift) - 1);
+                lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
+                lf_i = tleaf ? first : lf_i;
+                cur = (pop & !tleaf) ? top : cur;
+                state = (pop & !tleaf) ? 2 : state;
+            } else if (state == 4) {
                 lf_i += n_step;                     // with two, the first never ends the list
                 // end of the leaf: second leaf child, `next`, or the stack (selects)
                 const bool end = lf_i == lf_e;
@@ -2126,6 +2164,67 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 cur = tonext ? lf_next : (pop ? top : cur);
                 state = (tonext | pop) ? 2 : state;
                 sp -= pop ? 1 : 0;
+            }
+        } else if (kGfBvh4 && (phase & 2) && state == 2) {   // 4-wide node steps of the collection
+#pragma unroll 1
+            for (int ks = 0; ks < kNodeSteps; ks++) {
+                const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
+                const float4 LX = n4[0], LY = n4[1], LZ = n4[2], HX = n4[3], HY = n4[4], HZ = n4[5];
+                const float4 LKf = n4[6], CNf = n4[7];
+                const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, ly[4] = {LY.x, LY.y, LY.z, LY.w};
+                const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
+                const float hy[4] = {HY.x, HY.y, HY.z, HY.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+                const int lk[4] = {__float_as_int(LKf.x), __float_as_int(LKf.y), __float_as_int(LKf.z),
+                                   __float_as_int(LKf.w)};
+                const int cn[4] = {__float_as_int(CNf.x), __float_as_int(CNf.y), __float_as_int(CNf.z),
+                                   __float_as_int(CNf.w)};
+                const float X = tmin + win;
+                const float bound = X + gf_slack(X, t_box);
+                const f3 oi = o * ninv;
+                float key[4];
+                int ent[4];
+                int nhit = 0;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    // the binary step's child test (node_slab_g) on each of the four boxes
+                    const float a0 = __builtin_fmaf(lx[c], ninv.x, -oi.x), b0 = __builtin_fmaf(hx[c], ninv.x, -oi.x);
+                    const float a1 = __builtin_fmaf(ly[c], ninv.y, -oi.y), b1 = __builtin_fmaf(hy[c], ninv.y, -oi.y);
+                    const float a2 = __builtin_fmaf(lz[c], ninv.z, -oi.z), b2 = __builtin_fmaf(hz[c], ninv.z, -oi.z);
+                    const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
+                    const float tn = fmaxf(fmaxf(e0, e1), e2);
+                    const float tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
+                    const float tx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
+                    const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tx <= bound);
+                    key[c] = h ? tn : __int_as_float(0x7f800000);
+                    ent[c] = cn[c] > 0 ? leaf_entry4(lk[c], cn[c]) : lk[c];
+                    nhit += h ? 1 : 0;
+                }
+                // nearest first: sort the four (entry, key) pairs by key (misses last, at +inf)
+                auto cas = [&](int a, int b) {
+                    const bool sw = key[b] < key[a];
+                    const float ka = key[a], kb = key[b];
+                    const int ea = ent[a], eb = ent[b];
+                    key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
+                    ent[a] = sw ? eb : ea; ent[b] = sw ? ea : eb;
+                };
+                cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+                // the farther hits go on the stack, farthest first (the nearer pop first)
+                if (nhit > 3) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[3]); sp++; }
+                if (nhit > 2) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[2]); sp++; }
+                if (nhit > 1) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[1]); sp++; }
+                const bool pop = (nhit == 0) & (sp > 0);
+                const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
+                collected = (nhit == 0) & (sp == 0);
+                sp -= pop ? 1 : 0;
+                const int nx = nhit > 0 ? ent[0] : top;       // the entry to go on with (when not collected)
+                const bool leaf = !collected & (nx < 0);
+                const int first = nx & ((1 << kLeafCountShift) - 1);
+                lf_i = leaf ? first : lf_i;
+                lf_e = leaf ? first + ((nx >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
+                cur = (!collected & !leaf) ? nx : cur;
+                state = leaf ? 4 : state;
+                if (state != 2 || collected) break;    // a leaf reached, or the collection done
+                if (kNodeMinLanes > 0 && __popcll(__ballot(state == 2 && !collected)) < kNodeMinLanes) break;
             }
         } else if ((phase & 2) && state == 2) {         // PT_NODE_STEP nodes of the collection (window t_min + win)
 #pragma unroll 1
@@ -2187,7 +2286,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 const ModelRec& M = models[im];
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = M.bvh_root;
+                cur = kGfBvh4 ? M.bvh4_root : M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2246,7 +2345,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             } else {                                    // not provably exact: next tier's collection
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = M.bvh_root;
+                cur = kGfBvh4 ? M.bvh4_root : M.bvh_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2531,6 +2630,27 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
 // slot j -- the RNG seed and the hit-buffer index -- is carried, not changed.
 // ---------------------------------------------------------------------------
 
+// Longest-first claim order (sort modes 9 / 10): the persistent traces' drain --
+// waves left with a few long rays once the claim counter is exhausted -- is
+// shortest when the expensive rays are claimed first.  A ray is expensive when
+// it reaches a heavy model (kp.sort_heavy: a BLAS of many triangles): class 0 when
+// it starts inside a heavy model's world box, 1 when its half-line enters one from
+// outside, 2 otherwise.  Only the claim order changes, never a result.
+__device__ __forceinline__ int ray_cost_class(const KParams& p, f3 o, f3 d) {
+    const f3 winv = node_inv(cull_inv(d));
+    int c = 2;
+    for (unsigned h = p.sort_heavy; h; h &= h - 1) {
+        const ModelRec& M = p.models[__ffs(h) - 1];
+        const bool inside = o.x >= M.wbox[0] && o.y >= M.wbox[1] && o.z >= M.wbox[2] && o.x <= M.wbox[3] &&
+                            o.y <= M.wbox[4] && o.z <= M.wbox[5];
+        float tn, tf;
+        node_slab(M.wbox, M.wbox + 3, o, winv, tn, tf);
+        const bool enters = (tn <= tf) & (tf >= 0.0f);
+        c = min(c, inside ? 0 : (enters ? 1 : 2));
+    }
+    return c;
+}
+
 __device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
     // octahedral direction map (u, v in [-1, 1]) quantized to 64 x 64, origin cell 16^3
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
@@ -2565,6 +2685,16 @@ __device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
             return (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) | (((z >> 1) & 1) << 9) | (((a >> 2) & 1) << 8) |
                    (((b >> 2) & 1) << 7) | ((x & 1) << 6) | ((y & 1) << 5) | ((z & 1) << 4) | (((a >> 1) & 1) << 3) |
                    (((b >> 1) & 1) << 2) | ((a & 1) << 1) | (b & 1);
+        }
+        case 9:   // cost class major (expensive rays claimed first), then mode 7's top 11 bits
+        case 10: {// two class bits: starts inside a heavy model's box / enters one / neither
+            const int a = iu >> 3, b = iv >> 3, x = ix >> 2, y = iy >> 2, z = iz >> 2;
+            const int k7 = (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) | (((z >> 1) & 1) << 9) |
+                           (((a >> 2) & 1) << 8) | (((b >> 2) & 1) << 7) | ((x & 1) << 6) | ((y & 1) << 5) |
+                           ((z & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) | ((a & 1) << 1) | (b & 1);
+            const int c = ray_cost_class(p, o, d);
+            return p.sort_mode == 9 ? ((c == 2) << 11) | (k7 >> 1)
+                                    : (c << 10) | (k7 >> 2);
         }
         case 8: { // interleaved, direction 16 x 16 and origin 2^3... : u3 v3 x0 y0 z0 u2 v2 u1 v1 u0 v0 + pad
             const int a = iu >> 2, b = iv >> 2, x = ix >> 3, y = iy >> 3, z = iz >> 3;
@@ -2785,6 +2915,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.voxels, vox.data(), vox.size() * sizeof(int2), stream));
     PT_HIP(upload(allocs, &kp.per_voxel, scene.per_voxel_data_pool.data(), scene.per_voxel_data_pool.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
+    kp.bvh4 = nullptr;
+    if (!scene.bvh4_nodes.empty())
+        PT_HIP(upload(allocs, &kp.bvh4, scene.bvh4_nodes.data(), scene.bvh4_nodes.size() * sizeof(Bvh4Node), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
 
@@ -2832,6 +2965,13 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         // value does not fail a render whose trace never reads it
         const bool gf_split = split_trace && cfg.accel == ACCEL_GRID_FAST;
         const bool bvh_split = split_trace && cfg.accel == ACCEL_BVH;
+        if (gf_split && kGfBvh4) {     // this build's k_trace_gf walks the 4-wide BLAS only
+            for (const ModelRec& m : scene.model_recs)
+                if (m.bvh_root >= 0 && (m.bvh4_root < 0 || scene.bvh4_nodes.empty())) {
+                    last_error = "grid_fast (4-wide build): a mesh has no 4-wide BLAS (leaf too large)";
+                    return -1;
+                }
+        }
         gf_flags = gff && gf_split ? std::atoi(gff) : 9;
         if (gf_flags != 8 && gf_flags != 9) { last_error = "PT_GF_FLAGS must be 8 or 9"; return -1; }
         // 9..12 instances: the default variants with room for 12 LDS model records (F | 32)
@@ -2840,6 +2980,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         if (scene.model_recs.size() > (size_t)kLdsModelsGf && !gf_wide_lds) gf_flags &= ~1;   // records stay global
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
+        const char* rpl = std::getenv("PT_TRACE_RPL");
+        kp.trace_rpl = rpl ? std::max(0, std::atoi(rpl)) : 0;
         const char* tf = std::getenv("PT_TRACE_FLAGS");
         kp.trace_flags = tf && bvh_split ? std::atoi(tf) : 11;
         if (kp.trace_flags != 10 && kp.trace_flags != 11) { last_error = "PT_TRACE_FLAGS must be 10 or 11"; return -1; }
@@ -2858,6 +3000,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
         const int w = wpc ? std::max(1, std::atoi(wpc)) : (npipes > 1 ? 8 : 20);
         trace_blocks = std::max(1, cus) * w;
+        const char* mb = std::getenv("PT_TRACE_MIN_WAVES_PER_CU");
+        kp.trace_min_blocks = std::max(1, cus) * (mb ? std::max(1, std::atoi(mb)) : 2);
         const bool spills = split_trace && cfg.accel == ACCEL_GRID_FAST;   // k_trace_gf's 12-entry LDS stack
         // drain continuations
         const char* dd = std::getenv("PT_DRAIN_DUMP");
@@ -2880,7 +3024,18 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* so = std::getenv("PT_SORT");
         // auto: key 7 for both persistent traces (bvh: 3421 -> 3571 Mrays/s at 8 waves per CU, 16 pipelines)
         const int want = so ? std::atoi(so) : cfg.ray_sort >= 0 ? cfg.ray_sort : 7;
-        kp.sort_mode = split_trace ? std::max(0, std::min(8, want)) : 0;
+        kp.sort_mode = split_trace ? std::max(0, std::min(10, want)) : 0;
+        // heavy models for the cost-class keys: BLAS of at least a quarter of the largest one's triangles
+        // (and at least 4096), so a scene of small meshes has none and modes 9 / 10 reduce to mode 7's order
+        {
+            int most = 0;
+            for (const ModelRec& m : scene.model_recs) most = std::max(most, m.tri_end - m.tri_start);
+            kp.sort_heavy = 0;
+            for (size_t i = 0; i < scene.model_recs.size() && i < 32; i++) {
+                const int nt = scene.model_recs[i].tri_end - scene.model_recs[i].tri_start;
+                if (nt >= 4096 && 4 * nt >= most) kp.sort_heavy |= 1u << i;
+            }
+        }
         float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
         for (const ModelRec& m : scene.model_recs)
             for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], m.wbox[a]); hi[a] = std::max(hi[a], m.wbox[3 + a]); }

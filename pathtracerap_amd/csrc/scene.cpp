@@ -602,7 +602,7 @@ void Scene::buildDeviceTables() {
         r.tri_start = mesh.triangle_indices.start_index;
         r.tri_end = mesh.triangle_indices.end_index;
         r.bvh_root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m.mesh_index];
-        r.pad0 = 0;
+        r.bvh4_root = mesh_bvh4_root.empty() ? -1 : mesh_bvh4_root[m.mesh_index];
         ModelShade& sh = model_shade[i];
         for (int k = 0; k < 3; k++) sh.color[k] = m.mat.color[k];
         sh.mat_type = m.mat.material_type;
@@ -712,6 +712,7 @@ int Scene::build(const int gd[3], bool with_bvh) {
     mesh_bvh_root.assign(meshes.size(), -1);
     if (with_bvh)
         for (size_t m = 0; m < meshes.size(); m++) buildBvh((int)m);
+    buildBvh4();
     buildDeviceTables();
     built = true;
     return 0;

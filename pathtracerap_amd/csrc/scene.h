@@ -95,6 +95,8 @@ public:
                                       // the triangle index and its packed grid voxel box (mn, mx; 10 bits/axis)
     std::vector<int> tri_vbox;        // 2 ints / triangle: packed computeVoxelIndex min / max
     std::vector<int> mesh_bvh_root;
+    std::vector<Bvh4Node> bvh4_nodes; // the same BLAS collapsed 4-wide (k_trace_gf), all meshes
+    std::vector<int> mesh_bvh4_root;  // -1: no 4-wide BLAS (empty mesh, or a leaf the encoding cannot hold)
 
     RenderSettings settings;          // optional RENDER block of the config
     std::string last_error;
@@ -106,6 +108,7 @@ private:
     void buildDeviceTables();
     void buildBvh(int mesh);
     int relayoutPairs(int n0, int root);       // sibling inner nodes side by side (bvh.cpp)
+    void buildBvh4();                          // 4-wide collapse of every mesh's binary BLAS (bvh.cpp)
     void world_box(const Model& m, const Mesh& mesh, int root, float* out) const;
 };
 

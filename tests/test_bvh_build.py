@@ -83,3 +83,54 @@ def test_depth_cap_on_degenerate_distribution(pt_mod):
     assert sum(c for _, c, _ in leaves) == n
 
 
+
+
+def _walk4(nodes, root):
+    """Leaves (first, count, box) and depth of a 4-wide BLAS (Bvh4Node rows)."""
+    ints = nodes.view(np.int32)
+    leaves, depth_max, seen = [], 0, set()
+    stack = [(root, 1)]
+    while stack:
+        n, d = stack.pop()
+        assert n not in seen            # a tree: every node reached once
+        seen.add(n)
+        depth_max = max(depth_max, d)
+        for c in range(4):
+            count = ints[n, 28 + c]
+            if count < 0:
+                continue
+            box = (nodes[n, [c, 4 + c, 8 + c]], nodes[n, [12 + c, 16 + c, 20 + c]])
+            if count == 0:
+                stack.append((ints[n, 24 + c], d + 1))
+            else:
+                leaves.append((ints[n, 24 + c], count, box))
+    return leaves, depth_max, seen
+
+
+@pytest.mark.parametrize("ntri", [10, 5000, 60000])
+def test_bvh4_collapse_keeps_every_leaf_box_bit_for_bit(pt_mod, ntri):
+    """The 4-wide BLAS (k_trace_gf's node steps) holds exactly the binary
+    BLAS's leaves, with the same boxes bit for bit, at half the depth; every
+    leaf fits the traversal stack's leaf encoding."""
+    from pathtracerap_amd.synthetic import torus_mesh
+    pos, nrm, tris = torus_mesh(ntri, seed=1)
+    s = pt_mod.Scene()
+    m = s.addMesh(pos, nrm, tris)
+    s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
+    s.build(bvh=True)
+    b, b4 = s.export_bvh(), s.export_bvh4()
+    leaves2, depth2 = _walk(b["nodes"], b["roots"][0])
+    assert b4["roots"][0] >= 0
+    leaves4, depth4, seen = _walk4(b4["nodes"], b4["roots"][0])
+    assert len(seen) == len(b4["nodes"])          # no orphan nodes
+    key = lambda lv: (lv[0], lv[1], lv[2][0].tobytes(), lv[2][1].tobytes())
+    assert sorted(map(key, leaves4)) == sorted(map(key, leaves2))
+    assert depth4 <= (depth2 + 1) // 2 + 1
+    assert max(c for _, c, _ in leaves4) <= 31 and max(f for f, _, _ in leaves4) < (1 << 26)
+
+
+def test_bvh4_roots_for_every_mesh_of_the_reference_scene(pt_mod):
+    s = pt_mod.Scene(REF_SCENE)
+    s.build(bvh=True)
+    b4 = s.export_bvh4()
+    assert (b4["roots"] >= 0).all() and len(b4["nodes"]) > 0
