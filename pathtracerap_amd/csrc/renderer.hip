@@ -56,6 +56,9 @@ constexpr int kBlock = 256;
 #ifndef PT_NODE_MINLANES
 #define PT_NODE_MINLANES 8    // k_trace_gf: the wave leaves a node step once fewer lanes than this are still at a node
 #endif
+#ifndef PT_NODE_STEP_1P
+#define PT_NODE_STEP_1P 4     // k_trace_gf in-place variant (one pipeline, F & 16): node visits per node step
+#endif
 #ifndef PT_NODE_STEP
 #define PT_NODE_STEP 8        // k_trace_gf: node visits per node step (lanes still at an inner node go on)
 #endif
@@ -1273,6 +1276,9 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
 #ifndef PT_BVH_NODE_STEP
 #define PT_BVH_NODE_STEP 4    // k_trace_bvh: node visits per node step (as PT_NODE_STEP)
 #endif
+#ifndef PT_BVH_BVH4
+#define PT_BVH_BVH4 1         // k_trace_bvh: node steps over the 4-wide BLAS (stack spills past kStack); 0: binary
+#endif
 #ifndef PT_BVH_SEL_MASK
 #define PT_BVH_SEL_MASK 1     // k_trace_bvh: PT_SEL_MASK's candidate mask for the main launch's select steps
 #endif
@@ -1283,7 +1289,7 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
 #define PT_BVH_SEL_W 4
 #endif
 #ifndef PT_BVH_MINWAVES
-#define PT_BVH_MINWAVES 5     // waves per SIMD the k_trace_bvh register allocation must allow (96 VGPRs, 1 spilled: +3 % over 4 waves)
+#define PT_BVH_MINWAVES 4     // waves per SIMD the k_trace_bvh register allocation must allow (4-wide nodes: 4 waves, no spills, +7 % over 5 with 7 spilled)
 #endif
 // Model records staged in LDS when the scene has at most this many: k_trace_gf
 // 8 (7168 B of lane state + 8 x 248 B = 9152 B per 64-lane workgroup), or 12 for
@@ -1301,6 +1307,10 @@ constexpr int kLdsModels = PT_LDS_MODELS_BVH;
 constexpr int kLdsModelsWide = 12;
 constexpr int kLdsModelsGf = PT_LDS_MODELS_GF;
 constexpr int kSpillEntries = 64;  // traversal-stack entries per lane beyond the LDS part (global spill)
+// a leaf child pushed on a 4-wide traversal stack (negative: told apart from node indices)
+__device__ __forceinline__ int leaf_entry4(int first, int count) {
+    return (int)(0x80000000u | ((unsigned)count << kLeafCountShift) | (unsigned)first);
+}
 
 // Drain continuations.  Once a persistent trace's pool is exhausted its waves
 // empty out: every lane whose ray is done idles until the wave's longest ray
@@ -1332,7 +1342,13 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModels) : 1;
     __shared__ ModelRec s_models[kModelsHere];
     int* stack = s_stack + threadIdx.x;
-    // (the binary BLAS's depth cap keeps the whole traversal stack in LDS: no spill area)
+    // the binary BLAS's depth cap keeps its whole traversal stack in LDS; the 4-wide traversal
+    // (up to three pushes per node) spills past kStack entries to this lane's global area
+    constexpr bool kBvh4 = PT_BVH_BVH4 != 0;
+    static_assert(!kBvh4 || 3 * ((kMaxBvhDepth + 1) / 2 + 1) + 1 <= kStack + kSpillEntries,
+                  "k_trace_bvh's 4-wide traversal stack (LDS + spill) too small");
+    int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
+    int* spill = p.spill + sbase;
     // level 0: the main launch; level l >= 1: the tail launch resuming level l - 1's records
     const size_t cfield = (size_t)p.cont_cap * kContFields;        // one record buffer
     const int* cin = p.cont + (size_t)((level - 1) & 1) * cfield;   // records this (tail) launch resumes
@@ -1406,6 +1422,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         cur = C[kCCur * cs]; sp = C[kCSp * cs];
                         lf_i = C[kCLfI * cs]; lf_e = C[kCLfE * cs]; lf2_i = C[kCLf2I * cs]; lf2_e = C[kCLf2E * cs];
                         lf_next = C[kCLfNext * cs];
+                        if (kBvh4) { sbase = C[kCSpill * cs]; spill = p.spill + sbase; }
                         best = __int_as_float(C[kCX * cs]); best_tri = C[(kCX + 1) * cs]; any = C[(kCX + 2) * cs] != 0;
 #pragma unroll 1
                         for (int q = 0; q < kStack; q++) stack[q * BS] = C[(kCX + 3 + q) * cs];
@@ -1501,7 +1518,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 C[(kCDw + 2) * cs] = __float_as_int(dw.z);
                 C[kCCur * cs] = cur; C[kCSp * cs] = sp;
                 C[kCLfI * cs] = lf_i; C[kCLfE * cs] = lf_e; C[kCLf2I * cs] = lf2_i; C[kCLf2E * cs] = lf2_e;
-                C[kCLfNext * cs] = lf_next;
+                C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = sbase;
                 C[kCX * cs] = __float_as_int(best); C[(kCX + 1) * cs] = best_tri; C[(kCX + 2) * cs] = any ? 1 : 0;
 #pragma unroll 1
                 for (int q = 0; q < kStack; q++) C[(kCX + 3 + q) * cs] = stack[q * BS];
@@ -1539,7 +1556,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 ninv = node_inv(inv);
-                cur = M.bvh_root;
+                cur = kBvh4 ? M.bvh4_root : M.bvh_root;
                 sp = 0;
                 best = kFMax;
                 best_tri = -1;
@@ -1569,7 +1586,20 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 }
             }
             lf_i = min(lf_i + PT_LEAF_STEP, lf_e);
-            {
+            if (kBvh4) {
+                // end of the leaf: the next stack entry, a leaf (encoded, < 0) or a node
+                const bool end = lf_i == lf_e;
+                const bool pop = end & (sp > 0);
+                model_done = end & (sp == 0);
+                const int top = spop_if<BS, kStack>(pop, stack, spill, p.spill_stride, sp - 1);
+                sp -= pop ? 1 : 0;
+                const bool tleaf = pop & (top < 0);
+                const int first = top & ((1 << kLeafCountShift) - 1);
+                lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
+                lf_i = tleaf ? first : lf_i;
+                cur = (pop & !tleaf) ? top : cur;
+                state = (pop & !tleaf) ? 2 : state;
+            } else {
                 // end of the leaf: second leaf child, `next`, or the stack (selects)
                 const bool end = lf_i == lf_e;
                 const bool second = end & (lf2_i < lf2_e);
@@ -1584,6 +1614,61 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 cur = tonext ? lf_next : (pop ? top : cur);
                 state = (tonext | pop) ? 2 : state;
                 sp -= pop ? 1 : 0;
+            }
+        } else if (kBvh4 && (phase & 2) && state == 2) {
+#pragma unroll 1
+            for (int ks = 0; ks < PT_BVH_NODE_STEP; ks++) {
+                // 4-wide node visits: every hit child in order of entry, nearest first
+                const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
+                const float4 LX = n4[0], LY = n4[1], LZ = n4[2], HX = n4[3], HY = n4[4], HZ = n4[5];
+                const float4 LKf = n4[6], CNf = n4[7];
+                const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, ly[4] = {LY.x, LY.y, LY.z, LY.w};
+                const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
+                const float hy[4] = {HY.x, HY.y, HY.z, HY.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+                const int lk[4] = {__float_as_int(LKf.x), __float_as_int(LKf.y), __float_as_int(LKf.z),
+                                   __float_as_int(LKf.w)};
+                const int cn[4] = {__float_as_int(CNf.x), __float_as_int(CNf.y), __float_as_int(CNf.z),
+                                   __float_as_int(CNf.w)};
+                const f3 oi = o * ninv;
+                float key[4];
+                int ent[4];
+                int nhit = 0;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    // node_slab on each of the four boxes, bvh_step's hit rule
+                    const float a0 = __builtin_fmaf(lx[c], ninv.x, -oi.x), b0 = __builtin_fmaf(hx[c], ninv.x, -oi.x);
+                    const float a1 = __builtin_fmaf(ly[c], ninv.y, -oi.y), b1 = __builtin_fmaf(hy[c], ninv.y, -oi.y);
+                    const float a2 = __builtin_fmaf(lz[c], ninv.z, -oi.z), b2 = __builtin_fmaf(hz[c], ninv.z, -oi.z);
+                    const float tn = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fminf(a2, b2));
+                    const float tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
+                    const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tn <= best);
+                    key[c] = h ? tn : __int_as_float(0x7f800000);
+                    ent[c] = cn[c] > 0 ? leaf_entry4(lk[c], cn[c]) : lk[c];
+                    nhit += h ? 1 : 0;
+                }
+                auto cas = [&](int a, int b) {
+                    const bool sw = key[b] < key[a];
+                    const float ka = key[a], kb = key[b];
+                    const int ea = ent[a], eb = ent[b];
+                    key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
+                    ent[a] = sw ? eb : ea; ent[b] = sw ? ea : eb;
+                };
+                cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+                if (nhit > 3) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[3]); sp++; }
+                if (nhit > 2) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[2]); sp++; }
+                if (nhit > 1) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[1]); sp++; }
+                const bool pop = (nhit == 0) & (sp > 0);
+                const int top = spop_if<BS, kStack>(pop, stack, spill, p.spill_stride, sp - 1);
+                model_done = (nhit == 0) & (sp == 0);
+                sp -= pop ? 1 : 0;
+                const int nx = nhit > 0 ? ent[0] : top;
+                const bool leaf = !model_done & (nx < 0);
+                const int first = nx & ((1 << kLeafCountShift) - 1);
+                lf_i = leaf ? first : lf_i;
+                lf_e = leaf ? first + ((nx >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
+                cur = (!model_done & !leaf) ? nx : cur;
+                state = leaf ? 4 : state;
+                if (state != 2 || model_done) break;
             }
         } else if ((phase & 2) && state == 2) {
 #pragma unroll 1
@@ -1697,9 +1782,6 @@ constexpr bool kGfBvh4 = PT_GF_BVH4 != 0;
 // 4-wide traversal: at most 3 pushes per node on a path of at most (kMaxBvhDepth + 1) / 2 + 1 nodes
 static_assert(!kGfBvh4 || 3 * ((kMaxBvhDepth + 1) / 2 + 1) + 1 <= kGfStack + kSpillEntries,
               "k_trace_gf's 4-wide traversal stack (LDS + spill) too small");
-__device__ __forceinline__ int leaf_entry4(int first, int count) {
-    return (int)(0x80000000u | ((unsigned)count << kLeafCountShift) | (unsigned)first);
-}
 
 // Test hook: the walk certificates against the exact walk on the same hit set.
 // k_trace_gf's main launch decides most walks by walk_certify_fast (and, where it
@@ -1809,9 +1891,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     // found once per ray so later select steps jump to the next candidate
     constexpr bool kSelMask = PT_SEL_MASK && !TAIL && (F & 1);
     // node steps: the in-place variant (F & 16: one pipeline, one launch alone on the chip)
-    // measured best at 6 visits without the minimum (0.537 vs 0.558 ms per launch); the
+    // measured best at 4 visits (4-wide nodes) without the minimum; the
     // hand-on variants of several pipelines at PT_NODE_STEP / PT_NODE_MINLANES
-    constexpr int kNodeSteps = (F & 16) ? 6 : PT_NODE_STEP;
+    constexpr int kNodeSteps = (F & 16) ? PT_NODE_STEP_1P : PT_NODE_STEP;
     constexpr int kNodeMinLanes = (F & 16) ? 0 : PT_NODE_MINLANES;
     int* stack = s_stack + threadIdx.x;
     int4* hs = s_hs + threadIdx.x;
@@ -2965,10 +3047,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         // value does not fail a render whose trace never reads it
         const bool gf_split = split_trace && cfg.accel == ACCEL_GRID_FAST;
         const bool bvh_split = split_trace && cfg.accel == ACCEL_BVH;
-        if (gf_split && kGfBvh4) {     // this build's k_trace_gf walks the 4-wide BLAS only
+        if ((gf_split && kGfBvh4) || (bvh_split && PT_BVH_BVH4)) {   // this build's traces walk the 4-wide BLAS only
             for (const ModelRec& m : scene.model_recs)
                 if (m.bvh_root >= 0 && (m.bvh4_root < 0 || scene.bvh4_nodes.empty())) {
-                    last_error = "grid_fast (4-wide build): a mesh has no 4-wide BLAS (leaf too large)";
+                    last_error = "4-wide build: a mesh has no 4-wide BLAS (a leaf too large for the stack encoding)";
                     return -1;
                 }
         }
@@ -3002,7 +3084,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         trace_blocks = std::max(1, cus) * w;
         const char* mb = std::getenv("PT_TRACE_MIN_WAVES_PER_CU");
         kp.trace_min_blocks = std::max(1, cus) * (mb ? std::max(1, std::atoi(mb)) : 2);
-        const bool spills = split_trace && cfg.accel == ACCEL_GRID_FAST;   // k_trace_gf's 12-entry LDS stack
+        // k_trace_gf's 12-entry LDS stack; k_trace_bvh's 4-wide traversal (up to three pushes per node)
+        const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (cfg.accel == ACCEL_BVH && PT_BVH_BVH4));
         // drain continuations
         const char* dd = std::getenv("PT_DRAIN_DUMP");
         kp.drain_dump = split_trace ? std::max(0, std::min(64, dd ? std::atoi(dd) : 16)) : 0;
