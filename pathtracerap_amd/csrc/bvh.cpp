@@ -282,6 +282,11 @@ int Scene::relayoutPairs(int n0, int root) {
 // kMaxLeafCount4 triangles, or a first index >= 2^kLeafCountShift) gets no
 // 4-wide BLAS (root -1) and k_trace_gf's binary node steps trace it.
 void Scene::buildBvh4() {
+    // PT_BVH4_OPEN=0: open the first inner slot instead of the largest (build experiments)
+    static const bool kOpenLargest = [] {
+        const char* e = std::getenv("PT_BVH4_OPEN");
+        return !(e && std::atoi(e) == 0);
+    }();
     bvh4_nodes.clear();
     mesh_bvh4_root.assign(meshes.size(), -1);
     if (bvh_nodes.empty()) return;
@@ -312,18 +317,27 @@ void Scene::buildBvh4() {
         const int r4 = alloc(root);
         for (size_t w = 0; w < work.size(); w++) {
             const int b = work[w].first, id = work[w].second;
+            // open inner slots, largest surface area first, until four slots are filled
+            // (a leaf child leaves room to open a grandchild as well)
             Slot slots[4];
             int ns = 0;
             const BvhNode nd = bvh_nodes[b];
-            for (int c = 0; c < 2; c++) {
-                const Slot s = child(nd, c);
-                if (s.count == 0) {
-                    const BvhNode g = bvh_nodes[s.link];
-                    slots[ns++] = child(g, 0);
-                    slots[ns++] = child(g, 1);
-                } else {
-                    slots[ns++] = s;
-                }
+            slots[ns++] = child(nd, 0);
+            slots[ns++] = child(nd, 1);
+            auto area = [](const Slot& s) {
+                const double dx = (double)s.hi[0] - s.lo[0], dy = (double)s.hi[1] - s.lo[1], dz = (double)s.hi[2] - s.lo[2];
+                return dx * dy + dy * dz + dz * dx;
+            };
+            while (ns < 4) {
+                int best = -1;
+                for (int c = 0; c < ns; c++)
+                    if (slots[c].count == 0 && (best < 0 || (kOpenLargest && area(slots[c]) > area(slots[best])))) best = c;
+                if (best < 0) break;
+                const BvhNode g = bvh_nodes[slots[best].link];
+                for (int c = best; c + 1 < ns; c++) slots[c] = slots[c + 1];   // keep the children's order
+                ns--;
+                slots[ns++] = child(g, 0);
+                slots[ns++] = child(g, 1);
             }
             Bvh4Node out;
             std::memset(&out, 0, sizeof out);

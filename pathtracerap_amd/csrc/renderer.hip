@@ -1345,7 +1345,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     // the binary BLAS's depth cap keeps its whole traversal stack in LDS; the 4-wide traversal
     // (up to three pushes per node) spills past kStack entries to this lane's global area
     constexpr bool kBvh4 = PT_BVH_BVH4 != 0;
-    static_assert(!kBvh4 || 3 * ((kMaxBvhDepth + 1) / 2 + 1) + 1 <= kStack + kSpillEntries,
+    static_assert(!kBvh4 || 3 * (kMaxBvhDepth + 1) + 1 <= kStack + kSpillEntries,
                   "k_trace_bvh's 4-wide traversal stack (LDS + spill) too small");
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
     int* spill = p.spill + sbase;
@@ -1779,8 +1779,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
 constexpr bool kGfBvh4 = PT_GF_BVH4 != 0;
-// 4-wide traversal: at most 3 pushes per node on a path of at most (kMaxBvhDepth + 1) / 2 + 1 nodes
-static_assert(!kGfBvh4 || 3 * ((kMaxBvhDepth + 1) / 2 + 1) + 1 <= kGfStack + kSpillEntries,
+// 4-wide traversal: at most 3 pushes per node on a path of at most kMaxBvhDepth + 1 nodes (an unopened
+// slot keeps its binary level, so a 4-wide path can be as long as a binary one)
+static_assert(!kGfBvh4 || 3 * (kMaxBvhDepth + 1) + 1 <= kGfStack + kSpillEntries,
               "k_trace_gf's 4-wide traversal stack (LDS + spill) too small");
 
 // Test hook: the walk certificates against the exact walk on the same hit set.
