@@ -526,6 +526,25 @@ def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, mo
     assert_bitexact(img, oimg, f"PT_DRAIN_DUMP={dump} PT_DRAIN_LEVELS={levels} {scene}")
 
 
+@pytest.mark.parametrize("accel", [1, 2])
+@pytest.mark.parametrize("rpl,minw", [("0", "2"), ("4", "2"), ("64", "1"), ("1000000", "1")])
+def test_main_launch_sized_to_the_rays_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, rpl, minw):
+    """PT_TRACE_RPL: a bounce whose rays come to fewer than rpl per lane runs only
+    that many waves of its main trace launch (at least PT_TRACE_MIN_WAVES_PER_CU
+    per CU); the rest exit at once.  Only which wave traces which ray changes:
+    images and segment counts stay the oracle's, down to one wave per CU."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_TRACE_RPL", rpl)
+    monkeypatch.setenv("PT_TRACE_MIN_WAVES_PER_CU", minw)
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=6000, seed=13, metallic=True))
+    s.build(bvh=True)
+    cfg = P.RenderConfig(width=211, height=97, iterations=3, max_bounces=7, accel=accel, pipelines=4)
+    img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+    assert seg == oseg
+    assert_bitexact(img, oimg, f"PT_TRACE_RPL={rpl}")
+
+
 @pytest.mark.parametrize("handon,wcap,pipes", [(1, None, 1), (1, None, 4), (0, None, 1), (0, None, 4), (1, 7, 4)])
 @pytest.mark.parametrize("scene", ["synthetic", "reference"])
 def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, handon, wcap, pipes, scene):
