@@ -3064,8 +3064,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* rf = std::getenv("PT_TRACE_REFILL");
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
         const char* rpl = std::getenv("PT_TRACE_RPL");
-        // 4 rays per lane: +2.4 % at configs[4] (16 bounces, sparse late bounces), neutral at configs[1]
-        kp.trace_rpl = rpl ? std::max(0, std::atoi(rpl)) : 4;
+        // 4 rays per lane: +2.4 % at configs[4] (16 bounces, sparse late bounces), neutral at configs[1];
+        // off with one pipeline, where a launch has the chip to itself (its idle waves cost nothing)
+        kp.trace_rpl = rpl ? std::max(0, std::atoi(rpl)) : (npipes > 1 ? 4 : 0);
         const char* tf = std::getenv("PT_TRACE_FLAGS");
         kp.trace_flags = tf && bvh_split ? std::atoi(tf) : 11;
         if (kp.trace_flags != 10 && kp.trace_flags != 11) { last_error = "PT_TRACE_FLAGS must be 10 or 11"; return -1; }
