@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 6
+#define PT_ABI_VERSION 7
 
 /* Primitive.h:70-79 Material::MaterialType */
 enum {
