@@ -114,9 +114,6 @@ int pt_scene_export_bvh(const pt_scene *s, float *nodes, int *refs, int *roots);
  * 4-wide root (-1: none).  Returns the node count (call with nodes = NULL to
  * size the buffer), < 0 on error. */
 int pt_scene_export_bvh4(const pt_scene *s, float *nodes, int *roots);
-/* The 4-wide BLAS quantized to 64-byte nodes (Bvh4QNode, 16 words each, the
- * same node indices): returns the node count, < 0 on error. */
-int pt_scene_export_bvh4q(const pt_scene *s, float *nodes);
 
 /* ---- Renderer ---- */
 pt_renderer *pt_renderer_create(const pt_render_config *cfg);

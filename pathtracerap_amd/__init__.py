@@ -88,7 +88,6 @@ EXPORTS = [
                                        _P_F, _P_I, _P_F, _P_I, _P_I]),
     ("pt_scene_export_bvh", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_I, _P_I]),
     ("pt_scene_export_bvh4", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_I]),
-    ("pt_scene_export_bvh4q", ctypes.c_int, [ctypes.c_void_p, _P_F]),
     ("pt_renderer_create", ctypes.c_void_p, [ctypes.POINTER(_Cfg)]),
     ("pt_renderer_set_stream", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("pt_renderer_bind_image", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -294,17 +293,6 @@ def _scene_export_bvh4(self) -> dict:
 
 
 Scene.export_bvh4 = _scene_export_bvh4
-
-
-def _scene_export_bvh4q(self) -> np.ndarray:
-    """The 64-byte quantized 4-wide nodes (Bvh4QNode: 16 words per node)."""
-    cnt = _err(lib().pt_scene_export_bvh4q(self._h, None), "export_bvh4q")
-    nodes = np.zeros((max(cnt, 1), 16), np.float32)
-    _err(lib().pt_scene_export_bvh4q(self._h, _fp(nodes)), "export_bvh4q")
-    return nodes[:cnt]
-
-
-Scene.export_bvh4q = _scene_export_bvh4q
 
 
 

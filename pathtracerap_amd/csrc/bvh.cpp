@@ -361,66 +361,4 @@ void Scene::buildBvh4() {
     }
 }
 
-// 8-bit child boxes per 4-wide node, rounded outward in exact arithmetic: for
-// every child, px + qlo * 2^e <= lo and px + qhi * 2^e >= hi per axis (q * 2^e
-// and the sums are exact in double).  A node whose boxes cannot be quantized
-// (non-finite, or an extent beyond 255 * 2^126) is flagged: all children pass.
-void Scene::quantizeBvh4() {
-    bvh4q_nodes.assign(bvh4_nodes.size(), Bvh4QNode());
-    for (size_t i = 0; i < bvh4_nodes.size(); i++) {
-        const Bvh4Node& n = bvh4_nodes[i];
-        Bvh4QNode q;
-        std::memset(&q, 0, sizeof q);
-        const float* lo[3] = {n.lox, n.loy, n.loz};
-        const float* hi[3] = {n.hix, n.hiy, n.hiz};
-        unsigned* qlo[3] = {&q.qlox, &q.qloy, &q.qloz};
-        unsigned* qhi[3] = {&q.qhix, &q.qhiy, &q.qhiz};
-        float* pp[3] = {&q.px, &q.py, &q.pz};
-        bool ok = true;
-        for (int c = 0; c < 4; c++) {
-            q.link[c] = n.link[c];
-            const unsigned cb = n.count[c] < 0 ? 0xFFu : (unsigned)n.count[c];
-            q.counts |= cb << (8 * c);
-        }
-        for (int a = 0; a < 3 && ok; a++) {
-            double mn = 1e300, mx = -1e300;
-            for (int c = 0; c < 4; c++) {
-                if (n.count[c] < 0) continue;
-                mn = std::min(mn, (double)lo[a][c]);
-                mx = std::max(mx, (double)hi[a][c]);
-            }
-            if (mn > mx) { *pp[a] = 0.0f; continue; }          // no child: nothing to encode
-            if (!std::isfinite(mn) || !std::isfinite(mx)) { ok = false; break; }
-            const float p0 = (float)mn;
-            const double p = (double)(p0 <= mn ? p0 : std::nextafter(p0, -INFINITY));
-            *pp[a] = (float)p;
-            int e = -126;
-            while (e < 127 && std::ldexp(255.0, e) < mx - p) e++;
-            for (;; e++) {
-                if (e > 126) { ok = false; break; }
-                const double sc = std::ldexp(1.0, e);
-                bool fits = true;
-                unsigned wl = 0, wh = 0;
-                for (int c = 0; c < 4; c++) {
-                    if (n.count[c] < 0) continue;
-                    double l = std::floor(((double)lo[a][c] - p) / sc), h = std::ceil(((double)hi[a][c] - p) / sc);
-                    while (l > 0 && p + l * sc > (double)lo[a][c]) l -= 1.0;
-                    while (p + h * sc < (double)hi[a][c]) h += 1.0;
-                    if (l < 0) l = 0;
-                    if (h > 255.0) { fits = false; break; }
-                    wl |= (unsigned)l << (8 * c);
-                    wh |= (unsigned)h << (8 * c);
-                }
-                if (!fits) continue;
-                *qlo[a] = wl;
-                *qhi[a] = wh;
-                q.exps |= (unsigned)(e + 127) << (8 * a);
-                break;
-            }
-        }
-        if (!ok) q.flags = 1;
-        bvh4q_nodes[i] = q;
-    }
-}
-
 }  // namespace pt

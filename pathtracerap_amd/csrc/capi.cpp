@@ -202,14 +202,6 @@ int pt_scene_export_bvh4(const pt_scene* s, float* nodes, int* roots) {
     return (int)S.bvh4_nodes.size();
 }
 
-int pt_scene_export_bvh4q(const pt_scene* s, float* nodes) {
-    if (!s) return set_err("null scene");
-    const pt::Scene& S = s->s;
-    if (nodes && !S.bvh4q_nodes.empty())
-        std::memcpy(nodes, S.bvh4q_nodes.data(), S.bvh4q_nodes.size() * sizeof(pt::Bvh4QNode));
-    return (int)S.bvh4q_nodes.size();
-}
-
 pt_renderer* pt_renderer_create(const pt_render_config* c) {
     if (!c) { set_err("null config"); return nullptr; }
     if (c->accel != PT_ACCEL_GRID && c->accel != PT_ACCEL_BVH && c->accel != PT_ACCEL_GRID_FAST) {

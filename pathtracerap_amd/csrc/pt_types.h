@@ -81,21 +81,6 @@ struct Bvh4Node {
     int count[4];
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
-// The 4-wide node quantized to 64 bytes: child boxes as 8-bit offsets from the
-// node's box corner (px, py, pz) in units of 2^e per axis, rounded outward
-// (the dequantized box always contains Bvh4Node's, so a traversal reaches
-// every triangle it did before).  Bytes c of qlo*/qhi* are child c's; counts
-// byte c: 0xFF empty, 0 inner, 1..31 leaf triangles.  exps: e_x | e_y << 8 |
-// e_z << 16 (each e + 127 as a float exponent field); flags 1: the boxes could
-// not be quantized (non-finite or huge), every child passes the box test.
-struct Bvh4QNode {
-    float px, py, pz;
-    unsigned exps;
-    unsigned qlox, qloy, qloz, qhix;
-    unsigned qhiy, qhiz, counts, flags;
-    int link[4];
-};
-static_assert(sizeof(Bvh4QNode) == 64, "Bvh4QNode layout");
 // Leaf children pushed on k_trace_gf's 4-wide traversal stack are encoded as
 // (1 << 31) | (count << kLeafCountShift) | first: count <= kMaxLeafCount4,
 // first < 2^kLeafCountShift (Scene::buildBvh4 checks both).

@@ -46,7 +46,6 @@ struct KParams {
     const int* per_voxel;
     const BvhNode* bvh;
     const Bvh4Node* bvh4;       // the same BLAS 4-wide (k_trace_gf node steps; nullptr when the scene has none)
-    const Bvh4QNode* bvh4q;     // the 4-wide BLAS quantized to 64-byte nodes (same indices)
     const int* bvh_tri;
     const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
     int* spill;                 // traversal-stack spill beyond the LDS entries, lane-minor

@@ -1779,10 +1779,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #endif
 constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
 constexpr bool kGfBvh4 = PT_GF_BVH4 != 0;
-#ifndef PT_GF_QNODE
-#define PT_GF_QNODE 0         // k_trace_gf's 4-wide node steps read the 64-byte quantized nodes (Bvh4QNode)
-#endif
-constexpr bool kGfQNode = kGfBvh4 && PT_GF_QNODE != 0;
 // 4-wide traversal: at most 3 pushes per node on a path of at most kMaxBvhDepth + 1 nodes (an unopened
 // slot keeps its binary level, so a 4-wide path can be as long as a binary one)
 static_assert(!kGfBvh4 || 3 * (kMaxBvhDepth + 1) + 1 <= kGfStack + kSpillEntries,
@@ -2255,36 +2251,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         } else if (kGfBvh4 && (phase & 2) && state == 2) {   // 4-wide node steps of the collection
 #pragma unroll 1
             for (int ks = 0; ks < kNodeSteps; ks++) {
-                float key[4];
-                int ent[4];
-                int nhit = 0;
-                const float X = tmin + win;
-                const float bound = X + gf_slack(X, t_box);
-#if PT_GF_QNODE
-                // 64-byte node: per axis t = q * (2^e / d) + (px - o) / d for the 8-bit offsets q
-                const float4* __restrict__ nq = reinterpret_cast<const float4*>(p.bvh4q) + 4 * (size_t)cur;
-                const float4 H0 = nq[0], H1 = nq[1], H2 = nq[2], H3 = nq[3];
-                const unsigned ex = __float_as_uint(H0.w);
-                const float Ax = __uint_as_float((ex & 0xFFu) << 23) * ninv.x;
-                const float Ay = __uint_as_float(((ex >> 8) & 0xFFu) << 23) * ninv.y;
-                const float Az = __uint_as_float(((ex >> 16) & 0xFFu) << 23) * ninv.z;
-                const float Bx = (H0.x - o.x) * ninv.x, By = (H0.y - o.y) * ninv.y, Bz = (H0.z - o.z) * ninv.z;
-                const unsigned qlx = __float_as_uint(H1.x), qly = __float_as_uint(H1.y), qlz = __float_as_uint(H1.z);
-                const unsigned qhx = __float_as_uint(H1.w), qhy = __float_as_uint(H2.x), qhz = __float_as_uint(H2.y);
-                const unsigned cnw = __float_as_uint(H2.z);
-                const bool all_pass = (__float_as_uint(H2.w) & 1u) != 0;
-                const int lk[4] = {__float_as_int(H3.x), __float_as_int(H3.y), __float_as_int(H3.z), __float_as_int(H3.w)};
-#pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const unsigned cb = (cnw >> (8 * c)) & 0xFFu;
-                    const int cnc = cb == 0xFFu ? -1 : (int)cb;
-                    auto q = [&](unsigned w) { return (float)((w >> (8 * c)) & 0xFFu); };
-                    float a0 = __builtin_fmaf(q(qlx), Ax, Bx), b0 = __builtin_fmaf(q(qhx), Ax, Bx);
-                    float a1 = __builtin_fmaf(q(qly), Ay, By), b1 = __builtin_fmaf(q(qhy), Ay, By);
-                    float a2 = __builtin_fmaf(q(qlz), Az, Bz), b2 = __builtin_fmaf(q(qhz), Az, Bz);
-                    if (all_pass) { a0 = a1 = a2 = -3.0e38f; b0 = b1 = b2 = 3.0e38f; }
-                    const int lkc = lk[c];
-#else
                 const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
                 const float4 LX = n4[0], LY = n4[1], LZ = n4[2], HX = n4[3], HY = n4[4], HZ = n4[5];
                 const float4 LKf = n4[6], CNf = n4[7];
@@ -2295,22 +2261,25 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                                    __float_as_int(LKf.w)};
                 const int cn[4] = {__float_as_int(CNf.x), __float_as_int(CNf.y), __float_as_int(CNf.z),
                                    __float_as_int(CNf.w)};
+                const float X = tmin + win;
+                const float bound = X + gf_slack(X, t_box);
                 const f3 oi = o * ninv;
+                float key[4];
+                int ent[4];
+                int nhit = 0;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     // the binary step's child test (node_slab_g) on each of the four boxes
                     const float a0 = __builtin_fmaf(lx[c], ninv.x, -oi.x), b0 = __builtin_fmaf(hx[c], ninv.x, -oi.x);
                     const float a1 = __builtin_fmaf(ly[c], ninv.y, -oi.y), b1 = __builtin_fmaf(hy[c], ninv.y, -oi.y);
                     const float a2 = __builtin_fmaf(lz[c], ninv.z, -oi.z), b2 = __builtin_fmaf(hz[c], ninv.z, -oi.z);
-                    const int cnc = cn[c], lkc = lk[c];
-#endif
                     const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
                     const float tn = fmaxf(fmaxf(e0, e1), e2);
                     const float tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
                     const float tx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
-                    const bool h = (cnc >= 0) & (tn <= tf) & (tf >= -kEps) & (tx <= bound);
+                    const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tx <= bound);
                     key[c] = h ? tn : __int_as_float(0x7f800000);
-                    ent[c] = cnc > 0 ? leaf_entry4(lkc, cnc) : lkc;
+                    ent[c] = cn[c] > 0 ? leaf_entry4(lk[c], cn[c]) : lk[c];
                     nhit += h ? 1 : 0;
                 }
                 // nearest first: sort the four (entry, key) pairs by key (misses last, at +inf)
@@ -3030,11 +2999,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.per_voxel, scene.per_voxel_data_pool.data(), scene.per_voxel_data_pool.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
     kp.bvh4 = nullptr;
-    kp.bvh4q = nullptr;
     if (!scene.bvh4_nodes.empty())
         PT_HIP(upload(allocs, &kp.bvh4, scene.bvh4_nodes.data(), scene.bvh4_nodes.size() * sizeof(Bvh4Node), stream));
-    if (!scene.bvh4q_nodes.empty())
-        PT_HIP(upload(allocs, &kp.bvh4q, scene.bvh4q_nodes.data(), scene.bvh4q_nodes.size() * sizeof(Bvh4QNode), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
 

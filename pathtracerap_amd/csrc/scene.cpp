@@ -713,7 +713,6 @@ int Scene::build(const int gd[3], bool with_bvh) {
     if (with_bvh)
         for (size_t m = 0; m < meshes.size(); m++) buildBvh((int)m);
     buildBvh4();
-    quantizeBvh4();
     buildDeviceTables();
     built = true;
     return 0;

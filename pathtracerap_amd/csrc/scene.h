@@ -97,7 +97,6 @@ public:
     std::vector<int> mesh_bvh_root;
     std::vector<Bvh4Node> bvh4_nodes; // the same BLAS collapsed 4-wide (k_trace_gf), all meshes
     std::vector<int> mesh_bvh4_root;  // -1: no 4-wide BLAS (empty mesh, or a leaf the encoding cannot hold)
-    std::vector<Bvh4QNode> bvh4q_nodes; // bvh4_nodes quantized to 64 bytes, same indices
 
     RenderSettings settings;          // optional RENDER block of the config
     std::string last_error;
@@ -110,7 +109,6 @@ private:
     void buildBvh(int mesh);
     int relayoutPairs(int n0, int root);       // sibling inner nodes side by side (bvh.cpp)
     void buildBvh4();                          // 4-wide collapse of every mesh's binary BLAS (bvh.cpp)
-    void quantizeBvh4();                       // bvh4q_nodes from bvh4_nodes (bvh.cpp)
     void world_box(const Model& m, const Mesh& mesh, int root, float* out) const;
 };
 

@@ -134,37 +134,3 @@ def test_bvh4_roots_for_every_mesh_of_the_reference_scene(pt_mod):
     s.build(bvh=True)
     b4 = s.export_bvh4()
     assert (b4["roots"] >= 0).all() and len(b4["nodes"]) > 0
-
-
-@pytest.mark.parametrize("ntri", [10, 5000, 60000])
-def test_bvh4_quantized_boxes_contain_the_exact_ones(pt_mod, ntri):
-    """Every child box of the 64-byte quantized 4-wide nodes, dequantized
-    exactly (px + q * 2^e), contains the float box of the 128-byte node, and
-    links / counts are the same: a traversal over them reaches every triangle."""
-    from pathtracerap_amd.synthetic import torus_mesh
-    pos, nrm, tris = torus_mesh(ntri, seed=3)
-    s = pt_mod.Scene()
-    m = s.addMesh(pos, nrm, tris)
-    s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
-    s.build(bvh=True)
-    n4 = s.export_bvh4()["nodes"]
-    q = s.export_bvh4q()
-    assert len(q) == len(n4)
-    qi = q.view(np.uint32)
-    cnt4 = n4.view(np.int32)[:, 28:32]
-    assert (qi[:, 11] & 1 == 0).all()                  # every node quantized (flags word)
-    assert (q.view(np.int32)[:, 12:16] == n4.view(np.int32)[:, 24:28]).all()
-    cb = (qi[:, 10:11] >> (8 * np.arange(4, dtype=np.uint32))) & 0xFF
-    assert (np.where(cb == 0xFF, -1, cb.astype(np.int64)) == cnt4).all()
-    for a in range(3):
-        p = q[:, a].astype(np.float64)
-        e = ((qi[:, 3] >> (8 * a)) & 0xFF).astype(np.int64) - 127
-        sc = np.ldexp(1.0, e)
-        lo = (qi[:, 4 + a:5 + a] >> (8 * np.arange(4, dtype=np.uint32))) & 0xFF
-        hw = (qi[:, 7, None] if a == 0 else qi[:, 8 + a - 1, None])
-        hi = (hw >> (8 * np.arange(4, dtype=np.uint32))) & 0xFF
-        dlo = p[:, None] + lo * sc[:, None]
-        dhi = p[:, None] + hi * sc[:, None]
-        live = cnt4 >= 0
-        assert (dlo[live] <= n4[:, 4 * a:4 * a + 4][live].astype(np.float64)).all()
-        assert (dhi[live] >= n4[:, 12 + 4 * a:16 + 4 * a][live].astype(np.float64)).all()
