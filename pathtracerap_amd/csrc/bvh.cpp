@@ -349,7 +349,10 @@ void Scene::buildBvh4() {
                 out.lox[c] = s.lo[0]; out.loy[c] = s.lo[1]; out.loz[c] = s.lo[2];
                 out.hix[c] = s.hi[0]; out.hiy[c] = s.hi[1]; out.hiz[c] = s.hi[2];
                 out.count[c] = s.count;
-                out.link[c] = s.count == 0 ? alloc(s.link) : s.link;   // binary index -> 4-wide index
+                // inner: binary index -> 4-wide index; leaf: the stack's leaf entry
+                out.link[c] = s.count == 0 ? alloc(s.link)
+                            : s.count > 0 ? (int)(0x80000000u | ((unsigned)s.count << kLeafCountShift) | (unsigned)s.link)
+                                          : s.link;
             }
             bvh4_nodes[id] = out;
         }

@@ -68,12 +68,14 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
 
-// 4-wide BLAS node for k_trace_gf's node steps: a binary node and its two
-// children collapsed, so one 128-byte fetch (one dependent round trip) tests
-// what the binary layout tests in two.  Child c's box is (lo*[c], hi*[c]);
-// count[c] -1 = empty, 0 = inner (link = Bvh4Node index), > 0 = leaf (link =
-// first bvh_tri_order entry).  The same boxes as the binary nodes: only the
-// number of fetches per traversal changes, never the set of triangles tested.
+// 4-wide BLAS node for the traces' node steps: a binary node and its children
+// collapsed, so one 128-byte fetch (one dependent round trip) tests what the
+// binary layout tests in two.  Child c's box is (lo*[c], hi*[c]); count[c] -1 =
+// empty, 0 = inner (link = Bvh4Node index), > 0 = leaf, whose link is already
+// the traversal stack's leaf entry (1 << 31) | count << kLeafCountShift | first
+// (first = its first bvh_tri_order entry), so a node step pushes links as they
+// are.  The same boxes as the binary nodes: only the number of fetches per
+// traversal changes, never the set of triangles tested.
 struct Bvh4Node {
     float lox[4], loy[4], loz[4];
     float hix[4], hiy[4], hiz[4];

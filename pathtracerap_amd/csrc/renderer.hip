@@ -34,6 +34,9 @@
 namespace pt {
 
 constexpr int kBlock = 256;
+#ifndef PT_SORT4
+#define PT_SORT4 1            // 4-wide node steps: order the hit children by entry (0: nearest first only)
+#endif
 #ifndef PT_STACK
 #define PT_STACK 24
 #endif
@@ -1643,7 +1646,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     const float tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
                     const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tn <= best);
                     key[c] = h ? tn : __int_as_float(0x7f800000);
-                    ent[c] = cn[c] > 0 ? leaf_entry4(lk[c], cn[c]) : lk[c];
+                    ent[c] = lk[c];                          // leaves come encoded (Bvh4Node)
                     nhit += h ? 1 : 0;
                 }
                 auto cas = [&](int a, int b) {
@@ -1653,7 +1656,16 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
                     ent[a] = sw ? eb : ea; ent[b] = sw ? ea : eb;
                 };
-                cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+                if (PT_SORT4) {
+                    cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+                } else {                                    // nearest first only; the rest in slot order
+                    cas(0, 1); cas(0, 2); cas(0, 3);
+                    const bool m1 = key[1] != __int_as_float(0x7f800000), m2 = key[2] != __int_as_float(0x7f800000);
+                    // compact the hits among slots 1..3 to the front (misses are at +inf)
+                    const int e1 = ent[1], e2 = ent[2], e3 = ent[3];
+                    ent[1] = m1 ? e1 : (m2 ? e2 : e3);
+                    ent[2] = m1 ? (m2 ? e2 : e3) : e3;
+                }
                 if (nhit > 3) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[3]); sp++; }
                 if (nhit > 2) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[2]); sp++; }
                 if (nhit > 1) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[1]); sp++; }
@@ -2279,7 +2291,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     const float tx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
                     const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tx <= bound);
                     key[c] = h ? tn : __int_as_float(0x7f800000);
-                    ent[c] = cn[c] > 0 ? leaf_entry4(lk[c], cn[c]) : lk[c];
+                    ent[c] = lk[c];                          // leaves come encoded (Bvh4Node)
                     nhit += h ? 1 : 0;
                 }
                 // nearest first: sort the four (entry, key) pairs by key (misses last, at +inf)
@@ -2290,7 +2302,16 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
                     ent[a] = sw ? eb : ea; ent[b] = sw ? ea : eb;
                 };
-                cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+                if (PT_SORT4) {
+                    cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+                } else {                                    // nearest first only; the rest in slot order
+                    cas(0, 1); cas(0, 2); cas(0, 3);
+                    const bool m1 = key[1] != __int_as_float(0x7f800000), m2 = key[2] != __int_as_float(0x7f800000);
+                    // compact the hits among slots 1..3 to the front (misses are at +inf)
+                    const int e1 = ent[1], e2 = ent[2], e3 = ent[3];
+                    ent[1] = m1 ? e1 : (m2 ? e2 : e3);
+                    ent[2] = m1 ? (m2 ? e2 : e3) : e3;
+                }
                 // the farther hits go on the stack, farthest first (the nearer pop first)
                 if (nhit > 3) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[3]); sp++; }
                 if (nhit > 2) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[2]); sp++; }

@@ -102,8 +102,10 @@ def _walk4(nodes, root):
             box = (nodes[n, [c, 4 + c, 8 + c]], nodes[n, [12 + c, 16 + c, 20 + c]])
             if count == 0:
                 stack.append((ints[n, 24 + c], d + 1))
-            else:
-                leaves.append((ints[n, 24 + c], count, box))
+            else:                          # a leaf's link is its stack entry: 1 << 31 | count << 26 | first
+                e = int(ints[n, 24 + c]) & 0xFFFFFFFF
+                assert e >> 31 == 1 and (e >> 26) & 31 == count
+                leaves.append((e & ((1 << 26) - 1), count, box))
     return leaves, depth_max, seen
 
 
@@ -126,7 +128,7 @@ def test_bvh4_collapse_keeps_every_leaf_box_bit_for_bit(pt_mod, ntri):
     key = lambda lv: (lv[0], lv[1], lv[2][0].tobytes(), lv[2][1].tobytes())
     assert sorted(map(key, leaves4)) == sorted(map(key, leaves2))
     assert depth4 <= depth2 and len(b4["nodes"]) <= len(b["nodes"])
-    assert max(c for _, c, _ in leaves4) <= 31 and max(f for f, _, _ in leaves4) < (1 << 26)
+    assert max(c for _, c, _ in leaves4) <= 31
 
 
 def test_bvh4_roots_for_every_mesh_of_the_reference_scene(pt_mod):
