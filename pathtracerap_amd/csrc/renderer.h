@@ -100,7 +100,7 @@ struct KParams {
 
 constexpr int kMaxBounceCounters = 64;
 constexpr int kDrainLevels = 4;          // most tail launches per trace (drain continuations)
-constexpr int kDiagCounters = 64;        // diagnostic counters after the per-bounce ones (PT_TRACE_STATS builds)
+constexpr int kDiagCounters = 96;        // diagnostic counters after the per-bounce ones (PT_TRACE_STATS builds)
 // segments[] slot counting persistent-trace waves that hit trace_iter_cap and left
 // rays untraced (their hit records are stale): any non-zero value invalidates the image
 constexpr int kTraceFaultCounter = 7 + kMaxBounceCounters;

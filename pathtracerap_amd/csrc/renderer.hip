@@ -2170,6 +2170,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const float4 A0 = p.bvh_tri_geom[3 * lf_i], B0 = p.bvh_tri_geom[3 * lf_i + 1], C0 = p.bvh_tri_geom[3 * lf_i + 2];
             const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
             const int n_step = i1 != lf_i ? 2 : 1;
+            if (PT_TRACE_STATS && (p.debug & 16)) atomicAdd(p.segments + 68 + kMaxBounceCounters, (unsigned long long)n_step);
             // Both tests first (pure), then the hits' insertions in leaf order: the loop
             // below runs only for lanes with a hit, and carries 4 values instead of 12.
             float t0 = 0.0f, t1 = 0.0f;
@@ -2313,6 +2314,14 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     ent[2] = m1 ? (m2 ? e2 : e3) : e3;
                 }
                 // the farther hits go on the stack, farthest first (the nearer pop first)
+                if (PT_TRACE_STATS && (p.debug & 16)) {   // slots 64..67: pushes, spilled pushes, node visits, hits
+                    const int np = max(nhit - 1, 0);
+                    const int ns = max(0, sp + np - kGfStack) - max(0, sp - kGfStack);
+                    atomicAdd(p.segments + 64 + kMaxBounceCounters, (unsigned long long)np);
+                    if (ns > 0) atomicAdd(p.segments + 65 + kMaxBounceCounters, (unsigned long long)ns);
+                    atomicAdd(p.segments + 66 + kMaxBounceCounters, 1ull);
+                    atomicAdd(p.segments + 67 + kMaxBounceCounters, (unsigned long long)nhit);
+                }
                 if (nhit > 3) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[3]); sp++; }
                 if (nhit > 2) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[2]); sp++; }
                 if (nhit > 1) { spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, ent[1]); sp++; }

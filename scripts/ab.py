@@ -74,7 +74,7 @@ def main():
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
-        allc = rs[v].segments_per_bounce(127)
+        allc = rs[v].segments_per_bounce(159)
         if allc[71]:
             it = allc[71]
             out[v]["trace_iters_per_wave_total"] = it
@@ -93,6 +93,13 @@ def main():
             out[v]["phase_iters_per_segment"] = {k: round(a / sg, 3) for k, (a, b) in ph.items()}
             out[v]["tail_iter_share"] = round(allc[78] / it, 3)          # slot 15: tail launches' wave-iterations
             out[v]["busy_lanes_per_tail_iter"] = round(allc[106] / max(allc[78], 1), 2)   # slot 43
+        if allc[129]:                                  # slots 64..68 (stats build, & 16): 4-wide node steps
+            sg = max(rs[v].segments(), 1)
+            out[v]["node4"] = {"visits_per_segment": round(allc[129] / sg, 2),
+                               "hit_children_per_visit": round(allc[130] / allc[129], 3),
+                               "pushes_per_visit": round(allc[127] / allc[129], 3),
+                               "spilled_push_share": round(allc[128] / max(allc[127], 1), 4),
+                               "tri_tests_per_segment": round(allc[131] / sg, 2)}
         if any(allc[110:114]):                         # slots 47..50 (k_scan, stats build): hand-on volume
             sg = max(rs[v].segments(), 1)
             out[v]["handons_per_segment"] = dict(zip(["drained_l0", "walk_handons", "deferred", "drained_l1"],
