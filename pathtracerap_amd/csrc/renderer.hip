@@ -3124,7 +3124,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
                       scene.model_recs.size() <= (size_t)kLdsModelsWide;
         if (scene.model_recs.size() > (size_t)kLdsModelsGf && !gf_wide_lds) gf_flags &= ~1;   // records stay global
         const char* rf = std::getenv("PT_TRACE_REFILL");
-        kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : 32;
+        // refill a wave once 32 lanes are idle (48 with one pipeline: +2.5 % at configs[1], where a
+        // launch has the chip to itself and fewer refills keep more lanes on rays in flight)
+        kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : (npipes > 1 ? 32 : 48);
         const char* rpl = std::getenv("PT_TRACE_RPL");
         // 4 rays per lane: +2.4 % at configs[4] (16 bounces, sparse late bounces), neutral at configs[1];
         // off with one pipeline, where a launch has the chip to itself (its idle waves cost nothing)
