@@ -28,7 +28,10 @@ int leaf_max() {
     }();
     return v;
 }
-constexpr int kBins = 16;
+#ifndef PT_BVH_BINS
+#define PT_BVH_BINS 16
+#endif
+constexpr int kBins = PT_BVH_BINS;   // binned-SAH buckets per axis
 constexpr int kMaxDepth = kMaxBvhDepth;   // pt_types.h: the kernels' LDS stacks are sized (and asserted) for it
 
 struct Box {
