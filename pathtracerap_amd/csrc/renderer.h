@@ -82,7 +82,6 @@ struct KParams {
     unsigned short* sort_key;           // per source index of the previous bounce's pool
     int sort_mode;                      // key layout (k_sort_hist); 0 = no sort
     float sort_lo[3], sort_sc[3];       // origin cell = (o - lo) * sc, scene world box
-    unsigned sort_heavy;                // sort modes 9 / 10: models whose BLAS makes a ray expensive (bit mask)
     int* iter_dev;                      // hipGraph replay: k_bounce's iteration id (its `iter` argument is -1)
     int* cont;                          // drain continuations: rays a persistent trace handed on (SoA, stride cont_cap)
     int cont_cap;

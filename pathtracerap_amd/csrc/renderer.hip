@@ -37,9 +37,6 @@ constexpr int kBlock = 256;
 #ifndef PT_NEARFAR
 #define PT_NEARFAR 1          // 4-wide node steps load each axis near / far planes by the slope sign (+1 %)
 #endif
-#ifndef PT_SORT4
-#define PT_SORT4 1            // 4-wide node steps: order the hit children by entry (0: nearest first only)
-#endif
 #ifndef PT_STACK
 #define PT_STACK 24
 #endif
@@ -1662,16 +1659,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
                     ent[a] = sw ? eb : ea; ent[b] = sw ? ea : eb;
                 };
-                if (PT_SORT4) {
-                    cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
-                } else {                                    // nearest first only; the rest in slot order
-                    cas(0, 1); cas(0, 2); cas(0, 3);
-                    const bool m1 = key[1] != __int_as_float(0x7f800000), m2 = key[2] != __int_as_float(0x7f800000);
-                    // compact the hits among slots 1..3 to the front (misses are at +inf)
-                    const int e1 = ent[1], e2 = ent[2], e3 = ent[3];
-                    ent[1] = m1 ? e1 : (m2 ? e2 : e3);
-                    ent[2] = m1 ? (m2 ? e2 : e3) : e3;
-                }
+                cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
                 if (nhit > 3) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[3]); sp++; }
                 if (nhit > 2) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[2]); sp++; }
                 if (nhit > 1) { spush_t<BS, kStack>(stack, spill, p.spill_stride, sp, ent[1]); sp++; }
@@ -2335,16 +2323,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
                     ent[a] = sw ? eb : ea; ent[b] = sw ? ea : eb;
                 };
-                if (PT_SORT4) {
-                    cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
-                } else {                                    // nearest first only; the rest in slot order
-                    cas(0, 1); cas(0, 2); cas(0, 3);
-                    const bool m1 = key[1] != __int_as_float(0x7f800000), m2 = key[2] != __int_as_float(0x7f800000);
-                    // compact the hits among slots 1..3 to the front (misses are at +inf)
-                    const int e1 = ent[1], e2 = ent[2], e3 = ent[3];
-                    ent[1] = m1 ? e1 : (m2 ? e2 : e3);
-                    ent[2] = m1 ? (m2 ? e2 : e3) : e3;
-                }
+                cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
                 // the farther hits go on the stack, farthest first (the nearer pop first)
                 if (PT_TRACE_STATS && (p.debug & 16)) {   // slots 64..67: pushes, spilled pushes, node visits, hits
                     const int np = max(nhit - 1, 0);
@@ -2775,27 +2754,6 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
 // slot j -- the RNG seed and the hit-buffer index -- is carried, not changed.
 // ---------------------------------------------------------------------------
 
-// Longest-first claim order (sort modes 9 / 10): the persistent traces' drain --
-// waves left with a few long rays once the claim counter is exhausted -- is
-// shortest when the expensive rays are claimed first.  A ray is expensive when
-// it reaches a heavy model (kp.sort_heavy: a BLAS of many triangles): class 0 when
-// it starts inside a heavy model's world box, 1 when its half-line enters one from
-// outside, 2 otherwise.  Only the claim order changes, never a result.
-__device__ __forceinline__ int ray_cost_class(const KParams& p, f3 o, f3 d) {
-    const f3 winv = node_inv(cull_inv(d));
-    int c = 2;
-    for (unsigned h = p.sort_heavy; h; h &= h - 1) {
-        const ModelRec& M = p.models[__ffs(h) - 1];
-        const bool inside = o.x >= M.wbox[0] && o.y >= M.wbox[1] && o.z >= M.wbox[2] && o.x <= M.wbox[3] &&
-                            o.y <= M.wbox[4] && o.z <= M.wbox[5];
-        float tn, tf;
-        node_slab(M.wbox, M.wbox + 3, o, winv, tn, tf);
-        const bool enters = (tn <= tf) & (tf >= 0.0f);
-        c = min(c, inside ? 0 : (enters ? 1 : 2));
-    }
-    return c;
-}
-
 __device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
     // octahedral direction map (u, v in [-1, 1]) quantized to 64 x 64, origin cell 16^3
     const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
@@ -2830,16 +2788,6 @@ __device__ __forceinline__ int sort_key(const KParams& p, f3 o, f3 d) {
             return (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) | (((z >> 1) & 1) << 9) | (((a >> 2) & 1) << 8) |
                    (((b >> 2) & 1) << 7) | ((x & 1) << 6) | ((y & 1) << 5) | ((z & 1) << 4) | (((a >> 1) & 1) << 3) |
                    (((b >> 1) & 1) << 2) | ((a & 1) << 1) | (b & 1);
-        }
-        case 9:   // cost class major (expensive rays claimed first), then mode 7's top 11 bits
-        case 10: {// two class bits: starts inside a heavy model's box / enters one / neither
-            const int a = iu >> 3, b = iv >> 3, x = ix >> 2, y = iy >> 2, z = iz >> 2;
-            const int k7 = (((x >> 1) & 1) << 11) | (((y >> 1) & 1) << 10) | (((z >> 1) & 1) << 9) |
-                           (((a >> 2) & 1) << 8) | (((b >> 2) & 1) << 7) | ((x & 1) << 6) | ((y & 1) << 5) |
-                           ((z & 1) << 4) | (((a >> 1) & 1) << 3) | (((b >> 1) & 1) << 2) | ((a & 1) << 1) | (b & 1);
-            const int c = ray_cost_class(p, o, d);
-            return p.sort_mode == 9 ? ((c == 2) << 11) | (k7 >> 1)
-                                    : (c << 10) | (k7 >> 2);
         }
         case 8: { // interleaved, direction 16 x 16 and origin 2^3... : u3 v3 x0 y0 z0 u2 v2 u1 v1 u0 v0 + pad
             const int a = iu >> 2, b = iv >> 2, x = ix >> 3, y = iy >> 3, z = iz >> 3;
@@ -3174,18 +3122,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* so = std::getenv("PT_SORT");
         // auto: key 7 for both persistent traces (bvh: 3421 -> 3571 Mrays/s at 8 waves per CU, 16 pipelines)
         const int want = so ? std::atoi(so) : cfg.ray_sort >= 0 ? cfg.ray_sort : 7;
-        kp.sort_mode = split_trace ? std::max(0, std::min(10, want)) : 0;
-        // heavy models for the cost-class keys: BLAS of at least a quarter of the largest one's triangles
-        // (and at least 4096), so a scene of small meshes has none and modes 9 / 10 reduce to mode 7's order
-        {
-            int most = 0;
-            for (const ModelRec& m : scene.model_recs) most = std::max(most, m.tri_end - m.tri_start);
-            kp.sort_heavy = 0;
-            for (size_t i = 0; i < scene.model_recs.size() && i < 32; i++) {
-                const int nt = scene.model_recs[i].tri_end - scene.model_recs[i].tri_start;
-                if (nt >= 4096 && 4 * nt >= most) kp.sort_heavy |= 1u << i;
-            }
-        }
+        kp.sort_mode = split_trace ? std::max(0, std::min(8, want)) : 0;
         float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
         for (const ModelRec& m : scene.model_recs)
             for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], m.wbox[a]); hi[a] = std::max(hi[a], m.wbox[3 + a]); }
