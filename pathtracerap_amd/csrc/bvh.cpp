@@ -347,7 +347,10 @@ void Scene::buildBvh4() {
             for (int c = 0; c < 4; c++) {
                 Slot s;
                 if (c < ns) s = slots[c];
-                else { for (int k = 0; k < 3; k++) { s.lo[k] = 1.0f; s.hi[k] = -1.0f; } s.link = -1; s.count = -1; }
+                else {   // an empty slot: an inverted infinite box, which every slab test misses
+                    for (int k = 0; k < 3; k++) { s.lo[k] = INFINITY; s.hi[k] = -INFINITY; }
+                    s.link = -1; s.count = -1;
+                }
                 if (s.count > 0 && (s.count > kMaxLeafCount4 || s.link >= (1 << kLeafCountShift))) fits = false;
                 out.lox[c] = s.lo[0]; out.loy[c] = s.lo[1]; out.loz[c] = s.lo[2];
                 out.hix[c] = s.hi[0]; out.hiy[c] = s.hi[1]; out.hiz[c] = s.hi[2];

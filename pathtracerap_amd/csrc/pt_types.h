@@ -71,7 +71,8 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
 // 4-wide BLAS node for the traces' node steps: a binary node and its children
 // collapsed, so one 128-byte fetch (one dependent round trip) tests what the
 // binary layout tests in two.  Child c's box is (lo*[c], hi*[c]); count[c] -1 =
-// empty, 0 = inner (link = Bvh4Node index), > 0 = leaf, whose link is already
+// empty (box lo = +inf, hi = -inf: the node steps' near / far slab test misses
+// it by itself, so they never load count), 0 = inner (link = Bvh4Node index), > 0 = leaf, whose link is already
 // the traversal stack's leaf entry (1 << 31) | count << kLeafCountShift | first
 // (first = its first bvh_tri_order entry), so a node step pushes links as they
 // are.  The same boxes as the binary nodes: only the number of fetches per

@@ -34,9 +34,6 @@
 namespace pt {
 
 constexpr int kBlock = 256;
-#ifndef PT_NEARFAR
-#define PT_NEARFAR 1          // 4-wide node steps load each axis near / far planes by the slope sign (+1 %)
-#endif
 #ifndef PT_STACK
 #define PT_STACK 24
 #endif
@@ -1623,19 +1620,18 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             for (int ks = 0; ks < PT_BVH_NODE_STEP; ks++) {
                 // 4-wide node visits: every hit child in order of entry, nearest first
                 const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
-                // each axis' near / far planes by the slope's sign (k_trace_gf's PT_NEARFAR): the
-                // same entry / exit values as node_slab's min / max, without them
+                // each axis' near / far planes by the slope's sign (as k_trace_gf): the same entry /
+                // exit values as node_slab's min / max, without them; empty slots (inverted
+                // infinite boxes) miss by themselves
                 const int ox = ninv.x < 0.0f ? 3 : 0, oy = ninv.y < 0.0f ? 3 : 0, oz = ninv.z < 0.0f ? 3 : 0;
                 const float4 NX = n4[ox], NY = n4[1 + oy], NZ = n4[2 + oz];
                 const float4 FX = n4[3 - ox], FY = n4[4 - oy], FZ = n4[5 - oz];
-                const float4 LKf = n4[6], CNf = n4[7];
+                const float4 LKf = n4[6];
                 const float pnx[4] = {NX.x, NX.y, NX.z, NX.w}, pny[4] = {NY.x, NY.y, NY.z, NY.w};
                 const float pnz[4] = {NZ.x, NZ.y, NZ.z, NZ.w}, pfx[4] = {FX.x, FX.y, FX.z, FX.w};
                 const float pfy[4] = {FY.x, FY.y, FY.z, FY.w}, pfz[4] = {FZ.x, FZ.y, FZ.z, FZ.w};
                 const int lk[4] = {__float_as_int(LKf.x), __float_as_int(LKf.y), __float_as_int(LKf.z),
                                    __float_as_int(LKf.w)};
-                const int cn[4] = {__float_as_int(CNf.x), __float_as_int(CNf.y), __float_as_int(CNf.z),
-                                   __float_as_int(CNf.w)};
                 const f3 oi = o * ninv;
                 float key[4];
                 int ent[4];
@@ -1647,7 +1643,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                                            __builtin_fmaf(pnz[c], ninv.z, -oi.z));
                     const float tf = fminf(fminf(__builtin_fmaf(pfx[c], ninv.x, -oi.x), __builtin_fmaf(pfy[c], ninv.y, -oi.y)),
                                            __builtin_fmaf(pfz[c], ninv.z, -oi.z));
-                    const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tn <= best);
+                    const bool h = (tn <= tf) & (tf >= -kEps) & (tn <= best);
                     key[c] = h ? tn : __int_as_float(0x7f800000);
                     ent[c] = lk[c];                          // leaves come encoded (Bvh4Node)
                     nhit += h ? 1 : 0;
@@ -2259,28 +2255,18 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
 #pragma unroll 1
             for (int ks = 0; ks < kNodeSteps; ks++) {
                 const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
-#if PT_NEARFAR
                 // per axis, the slab a child is entered through is fixed by the sign of the slope:
                 // load each axis' near and far planes directly (lo for a positive slope), so the
                 // entries and exits come without min / max, and the voxel-grown entry is one fma
                 const int ox = ninv.x < 0.0f ? 3 : 0, oy = ninv.y < 0.0f ? 3 : 0, oz = ninv.z < 0.0f ? 3 : 0;
                 const float4 NX = n4[ox], NY = n4[1 + oy], NZ = n4[2 + oz];
                 const float4 FX = n4[3 - ox], FY = n4[4 - oy], FZ = n4[5 - oz];
-                const float4 LKf = n4[6], CNf = n4[7];
+                const float4 LKf = n4[6];
                 const float pnx[4] = {NX.x, NX.y, NX.z, NX.w}, pny[4] = {NY.x, NY.y, NY.z, NY.w};
                 const float pnz[4] = {NZ.x, NZ.y, NZ.z, NZ.w}, pfx[4] = {FX.x, FX.y, FX.z, FX.w};
                 const float pfy[4] = {FY.x, FY.y, FY.z, FY.w}, pfz[4] = {FZ.x, FZ.y, FZ.z, FZ.w};
-#else
-                const float4 LX = n4[0], LY = n4[1], LZ = n4[2], HX = n4[3], HY = n4[4], HZ = n4[5];
-                const float4 LKf = n4[6], CNf = n4[7];
-                const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, ly[4] = {LY.x, LY.y, LY.z, LY.w};
-                const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
-                const float hy[4] = {HY.x, HY.y, HY.z, HY.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
-#endif
                 const int lk[4] = {__float_as_int(LKf.x), __float_as_int(LKf.y), __float_as_int(LKf.z),
                                    __float_as_int(LKf.w)};
-                const int cn[4] = {__float_as_int(CNf.x), __float_as_int(CNf.y), __float_as_int(CNf.z),
-                                   __float_as_int(CNf.w)};
                 const float X = tmin + win;
                 const float bound = X + gf_slack(X, t_box);
                 const f3 oi = o * ninv;
@@ -2289,9 +2275,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 int nhit = 0;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
-#if PT_NEARFAR
-                    // tn / tf: the same fma values as the min / max below; tx: the grown entry
-                    // with the growth folded into the offset (within gf_slack of e - G)
+                    // tn / tf: the same fma values as node_slab_g's min / max pick; tx: the grown
+                    // entry with the growth folded into the offset (within gf_slack of e - G).  An
+                    // empty slot's inverted infinite box gives tn = +inf, tf = -inf: a miss, so
+                    // Bvh4Node.count is never loaded
                     const float e0 = __builtin_fmaf(pnx[c], ninv.x, -oi.x), e1 = __builtin_fmaf(pny[c], ninv.y, -oi.y);
                     const float e2 = __builtin_fmaf(pnz[c], ninv.z, -oi.z);
                     const float tn = fmaxf(fmaxf(e0, e1), e2);
@@ -2300,17 +2287,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     const float tx = fmaxf(fmaxf(__builtin_fmaf(pnx[c], ninv.x, -(oi.x + G.x)),
                                                  __builtin_fmaf(pny[c], ninv.y, -(oi.y + G.y))),
                                            __builtin_fmaf(pnz[c], ninv.z, -(oi.z + G.z)));
-#else
-                    // the binary step's child test (node_slab_g) on each of the four boxes
-                    const float a0 = __builtin_fmaf(lx[c], ninv.x, -oi.x), b0 = __builtin_fmaf(hx[c], ninv.x, -oi.x);
-                    const float a1 = __builtin_fmaf(ly[c], ninv.y, -oi.y), b1 = __builtin_fmaf(hy[c], ninv.y, -oi.y);
-                    const float a2 = __builtin_fmaf(lz[c], ninv.z, -oi.z), b2 = __builtin_fmaf(hz[c], ninv.z, -oi.z);
-                    const float e0 = fminf(a0, b0), e1 = fminf(a1, b1), e2 = fminf(a2, b2);
-                    const float tn = fmaxf(fmaxf(e0, e1), e2);
-                    const float tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
-                    const float tx = fmaxf(fmaxf(e0 - G.x, e1 - G.y), e2 - G.z);
-#endif
-                    const bool h = (cn[c] >= 0) & (tn <= tf) & (tf >= -kEps) & (tx <= bound);
+                    const bool h = (tn <= tf) & (tf >= -kEps) & (tx <= bound);
                     key[c] = h ? tn : __int_as_float(0x7f800000);
                     ent[c] = lk[c];                          // leaves come encoded (Bvh4Node)
                     nhit += h ? 1 : 0;

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/../.."
 V=(
  "default|"
  "binary BLAS (ab_bvh4)|-DPT_GF_BVH4=0 -DPT_BVH_BVH4=0"
- "near/far off (ab_nearfar)|-DPT_NEARFAR=0"
+ "near/far off (ab_nearfar; switch removed with the count-free node step)|-DPT_NEARFAR=0"
  "node step 4 (ab_nodestep4_bvh)|-DPT_NODE_STEP=4"
  "node step 6|-DPT_NODE_STEP=6"
  "node step 12|-DPT_NODE_STEP=12"
