@@ -9,7 +9,7 @@ T=build_variants/src_$NAME
 rm -rf $T && mkdir -p $T
 git archive "$REV" pathtracerap_amd/csrc include | tar -x -C $T
 cd $T/pathtracerap_amd && mkdir -p o
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wno-unused-result -Wno-unused-value -Wno-pass-failed $D"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-result -Wno-unused-value -Wno-pass-failed $D"
 for s in scene bvh capi; do /opt/rocm/bin/hipcc $F -x hip -c csrc/$s.cpp -o o/$s.o & done
 /opt/rocm/bin/hipcc $F -c csrc/renderer.hip -o o/renderer.o
 wait

@@ -7,7 +7,7 @@ NAME=$1; shift
 D="$*"
 OUT=../build_variants/obj_$NAME
 mkdir -p $OUT
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wno-unused-result -Wno-unused-value -Wno-pass-failed $D"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wno-unused-result -Wno-unused-value -Wno-pass-failed $D"
 for s in scene bvh capi; do /opt/rocm/bin/hipcc $F -x hip -c csrc/$s.cpp -o $OUT/$s.o & done
 /opt/rocm/bin/hipcc $F -c csrc/renderer.hip -o $OUT/renderer.o
 wait
