@@ -1254,10 +1254,35 @@ __device__ __forceinline__ int slot_source(const KParams& p, int j) {
 // Every wave exits once all blocks are claimed and its lanes are idle.
 // Per-lane traversal stack: kStack entries in LDS (lane-contiguous), deeper
 // entries in a global spill area laid out lane-minor (p.spill_stride lanes).
+// The seven float4 loads of a 4-wide node visit (Bvh4Node: planes lo x/y/z, hi x/y/z,
+// links; count is never read): each axis' near and far planes by the slope sign's
+// offset o* (0 or 3).  PT_NODE_OFF32: 32-bit byte offsets from the node array's base,
+// so the loads take the SGPR base + 32-bit VGPR offset form (one 32-bit add per
+// plane instead of a 64-bit address each; the BLAS is < 4 GB: leaf entries cap a
+// mesh at 2^26 triangles).
+#ifndef PT_NODE_OFF32
+#define PT_NODE_OFF32 1
+#endif
+#if PT_NODE_OFF32
+#define PT_NODE_LOADS(cur, ox, oy, oz)                                                                   \
+    const char* __restrict__ nb_ = reinterpret_cast<const char*>(p.bvh4);                                \
+    const unsigned nbo_ = (unsigned)(cur) << 7;                                                          \
+    auto ld4_ = [&](int q) { return *reinterpret_cast<const float4*>(nb_ + (nbo_ + 16u * (unsigned)q)); }; \
+    const float4 NX = ld4_(ox), NY = ld4_(1 + (oy)), NZ = ld4_(2 + (oz));                                \
+    const float4 FX = ld4_(3 - (ox)), FY = ld4_(4 - (oy)), FZ = ld4_(5 - (oz));                          \
+    const float4 LKf = ld4_(6);
+#else
+#define PT_NODE_LOADS(cur, ox, oy, oz)                                                                   \
+    const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)(cur);         \
+    const float4 NX = n4[ox], NY = n4[1 + (oy)], NZ = n4[2 + (oz)];                                      \
+    const float4 FX = n4[3 - (ox)], FY = n4[4 - (oy)], FZ = n4[5 - (oz)];                                \
+    const float4 LKf = n4[6];
+#endif
+
 template <int BS, int SCAP = kStack>
 __device__ __forceinline__ void spush_t(int* stack, int* spill, int stride, int sp, int e) {
     if (sp < SCAP) stack[sp * BS] = e;
-    else spill[(size_t)(sp - SCAP) * stride] = e;
+    else spill[(sp - SCAP) * stride] = e;     // 32-bit: allocPipe keeps the spill area under 2^31 entries
 }
 // Pop for the lanes with `take`, without a branch around the LDS read: every lane
 // reads its (clamped) LDS entry; only a spilled entry is read under a branch.
@@ -1266,7 +1291,7 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
     typedef __attribute__((address_space(3))) const int lds_int;
     typedef __attribute__((address_space(1))) const int glb_int;
     int v = ((lds_int*)stack)[min(max(sp, 0), SCAP - 1) * BS];
-    if (take & (sp >= SCAP)) v = ((glb_int*)spill)[(size_t)(sp - SCAP) * stride];
+    if (take & (sp >= SCAP)) v = ((glb_int*)spill)[(sp - SCAP) * stride];
     return v;
 }
 
@@ -1619,14 +1644,11 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #pragma unroll 1
             for (int ks = 0; ks < PT_BVH_NODE_STEP; ks++) {
                 // 4-wide node visits: every hit child in order of entry, nearest first
-                const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
                 // each axis' near / far planes by the slope's sign (as k_trace_gf): the same entry /
                 // exit values as node_slab's min / max, without them; empty slots (inverted
                 // infinite boxes) miss by themselves
                 const int ox = ninv.x < 0.0f ? 3 : 0, oy = ninv.y < 0.0f ? 3 : 0, oz = ninv.z < 0.0f ? 3 : 0;
-                const float4 NX = n4[ox], NY = n4[1 + oy], NZ = n4[2 + oz];
-                const float4 FX = n4[3 - ox], FY = n4[4 - oy], FZ = n4[5 - oz];
-                const float4 LKf = n4[6];
+                PT_NODE_LOADS(cur, ox, oy, oz)
                 const float pnx[4] = {NX.x, NX.y, NX.z, NX.w}, pny[4] = {NY.x, NY.y, NY.z, NY.w};
                 const float pnz[4] = {NZ.x, NZ.y, NZ.z, NZ.w}, pfx[4] = {FX.x, FX.y, FX.z, FX.w};
                 const float pfy[4] = {FY.x, FY.y, FY.z, FY.w}, pfz[4] = {FZ.x, FZ.y, FZ.z, FZ.w};
@@ -2254,14 +2276,11 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         } else if (kGfBvh4 && (phase & 2) && state == 2) {   // 4-wide node steps of the collection
 #pragma unroll 1
             for (int ks = 0; ks < kNodeSteps; ks++) {
-                const float4* __restrict__ n4 = reinterpret_cast<const float4*>(p.bvh4) + 8 * (size_t)cur;
                 // per axis, the slab a child is entered through is fixed by the sign of the slope:
                 // load each axis' near and far planes directly (lo for a positive slope), so the
                 // entries and exits come without min / max, and the voxel-grown entry is one fma
                 const int ox = ninv.x < 0.0f ? 3 : 0, oy = ninv.y < 0.0f ? 3 : 0, oz = ninv.z < 0.0f ? 3 : 0;
-                const float4 NX = n4[ox], NY = n4[1 + oy], NZ = n4[2 + oz];
-                const float4 FX = n4[3 - ox], FY = n4[4 - oy], FZ = n4[5 - oz];
-                const float4 LKf = n4[6];
+                PT_NODE_LOADS(cur, ox, oy, oz)
                 const float pnx[4] = {NX.x, NX.y, NX.z, NX.w}, pny[4] = {NY.x, NY.y, NY.z, NY.w};
                 const float pnz[4] = {NZ.x, NZ.y, NZ.z, NZ.w}, pfx[4] = {FX.x, FX.y, FX.z, FX.w};
                 const float pfy[4] = {FY.x, FY.y, FY.z, FY.w}, pfz[4] = {FZ.x, FZ.y, FZ.z, FZ.w};
@@ -3160,6 +3179,10 @@ int Renderer::allocPipe(KParams& k, size_t cap, hipStream_t st) {
     PT_HIP(upload(allocs, &k.hs_pool, nullptr, (size_t)k.hs_pool_blocks * kHitCapPool * sizeof(int4), st));
     PT_HIP(upload(allocs, &k.hs_pool_next, nullptr, sizeof(int), st));
     PT_HIP(hipMemsetAsync(k.hs_pool_next, 0, sizeof(int), st));
+    if ((size_t)k.spill_stride * kSpillEntries >= (1ull << 31)) {   // spush_t / spop_if index it in 32 bits
+        last_error = "traversal spill area too large";
+        return -1;
+    }
     PT_HIP(upload(allocs, &k.spill, nullptr, (size_t)k.spill_stride * kSpillEntries * sizeof(int), st));
     const size_t dcap = split_trace && cfg.accel == ACCEL_GRID_FAST ? cap : 1;
     PT_HIP(upload(allocs, &k.defer_slots, nullptr, dcap * sizeof(int), st));
