@@ -1263,21 +1263,6 @@ __device__ __forceinline__ int slot_source(const KParams& p, int j) {
 #ifndef PT_NODE_OFF32
 #define PT_NODE_OFF32 1
 #endif
-// A leaf triangle's three float4 (bvh_tri_geom: v0 + index, edge 1 + voxel box lo,
-// edge 2 + voxel box hi) at a 32-bit byte offset from the array's base (< 4 GB:
-// 2^26 triangles x 48 B at most), SGPR-base loads as the node loads.
-#if PT_NODE_OFF32
-#define PT_TRI_LOADS(i, A, B, C)                                                                         \
-    {                                                                                                    \
-        const char* __restrict__ tb_ = reinterpret_cast<const char*>(p.bvh_tri_geom);                   \
-        const unsigned to_ = (unsigned)(i) * 48u;                                                        \
-        A = *reinterpret_cast<const float4*>(tb_ + to_);                                                 \
-        B = *reinterpret_cast<const float4*>(tb_ + (to_ + 16u));                                         \
-        C = *reinterpret_cast<const float4*>(tb_ + (to_ + 32u));                                         \
-    }
-#else
-#define PT_TRI_LOADS(i, A, B, C) { A = p.bvh_tri_geom[3 * (i)]; B = p.bvh_tri_geom[3 * (i) + 1]; C = p.bvh_tri_geom[3 * (i) + 2]; }
-#endif
 #if PT_NODE_OFF32
 #define PT_NODE_LOADS(cur, ox, oy, oz)                                                                   \
     const char* __restrict__ nb_ = reinterpret_cast<const char*>(p.bvh4);                                \
@@ -1613,7 +1598,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #pragma unroll
             for (int q = 0; q < PT_LEAF_STEP; q++) {
                 const int iq = lf_i + q < lf_e ? lf_i + q : lf_i;
-                PT_TRI_LOADS(iq, TA[q], TB[q], TC[q])
+                TA[q] = p.bvh_tri_geom[3 * iq]; TB[q] = p.bvh_tri_geom[3 * iq + 1]; TC[q] = p.bvh_tri_geom[3 * iq + 2];
             }
 #pragma unroll
             for (int q = 0; q < PT_LEAF_STEP; q++) {
@@ -1812,9 +1797,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #endif
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
-#endif
-#ifndef PT_PRIO
-#define PT_PRIO 0             // k_trace_gf: wave priority (s_setprio) during node and leaf steps (0: never raised)
 #endif
 #ifndef PT_GF_BVH4
 #define PT_GF_BVH4 1          // k_trace_gf: node steps over the 4-wide BLAS (Bvh4Node); 0: the binary one
@@ -2193,16 +2175,12 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         }
         if (stamps) { const unsigned long long t = clock64(); cy[1] += t - ts; ts = t; }
         bool collected = false;
-        // PT_PRIO: node and leaf steps (a burst of loads, then short ALU work) at a raised wave
-        // priority, so a wave about to issue its loads wins the SIMD over ALU-bound walk phases
-        if (PT_PRIO > 0 && (phase & 6)) __builtin_amdgcn_s_setprio(PT_PRIO);
         if ((phase & 4) && state == 4) {                // leaf triangles of the collection: up to PT_LEAF_STEP
             // per step, their loads issued together; tested in leaf order, as one per step would
             // (k_trace_gf: at most two -- selecting from a longer array spilled 33+ VGPRs)
             const int i1 = (PT_LEAF_STEP > 1 && lf_i + 1 < lf_e) ? lf_i + 1 : lf_i;
-            float4 A0, B0, C0, A1, B1, C1;
-            PT_TRI_LOADS(lf_i, A0, B0, C0)
-            PT_TRI_LOADS(i1, A1, B1, C1)
+            const float4 A0 = p.bvh_tri_geom[3 * lf_i], B0 = p.bvh_tri_geom[3 * lf_i + 1], C0 = p.bvh_tri_geom[3 * lf_i + 2];
+            const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
             const int n_step = i1 != lf_i ? 2 : 1;
             if (PT_TRACE_STATS && (p.debug & 16)) atomicAdd(p.segments + 68 + kMaxBounceCounters, (unsigned long long)n_step);
             // Both tests first (pure), then the hits' insertions in leaf order: the loop
@@ -2416,7 +2394,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 if (kNodeMinLanes > 0 && __popcll(__ballot(state == 2 && !collected)) < kNodeMinLanes) break;
             }
         }
-        if (PT_PRIO > 0 && (phase & 6)) __builtin_amdgcn_s_setprio(0);
         if (stamps) { const unsigned long long t = clock64(); cy[(phase & 4) ? 2 : 3] += t - ts; ts = t; }
         if (collected) {
             if (nh > 0) {
