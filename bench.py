@@ -451,7 +451,7 @@ def trace_roofline(stats1, per_bounce, K, elapsed, ms_per_step, kname, workload_
             "kernel": kname, "workload_key": workload_key,
             "basis": "per launch: algorithmic bytes of one bounce's trace (52 B x segments entering the bounce) "
                      "/ its average duration, HIP events on the launch stream, one pipeline (rocprofv3: "
-                     "profiles/r05/kernel_stats_*_1p.csv); traffic = PMC HBM bytes per launch of the same "
+                     "profiles/r06/kernel_stats_*_1p.csv); traffic = PMC HBM bytes per launch of the same "
                      "command, (2 FETCH_SIZE + WRITE_SIZE) KiB (profiles/pmc_latest.json)",
             "algorithmic_bytes_per_launch": round(b_launch), "avg_launch_ms": round(k1, 4),
             "launches": l1, "trace_phases_per_step": phases,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 7
+#define PT_ABI_VERSION 8
 
 /* Primitive.h:70-79 Material::MaterialType */
 enum {
@@ -114,6 +114,10 @@ int pt_scene_export_bvh(const pt_scene *s, float *nodes, int *refs, int *roots);
  * 4-wide root (-1: none).  Returns the node count (call with nodes = NULL to
  * size the buffer), < 0 on error. */
 int pt_scene_export_bvh4(const pt_scene *s, float *nodes, int *roots);
+/* Each mesh's first leaf record (bvh_tri_order entry), nmesh ints: a 4-wide
+ * leaf link (1 << 31 | count << 26 | first) holds first relative to it, so
+ * the 2^26 limit of the encoding is per mesh (ABI 8).  Returns nmesh. */
+int pt_scene_export_bvh4_leaf_base(const pt_scene *s, int *bases);
 
 /* ---- Renderer ---- */
 pt_renderer *pt_renderer_create(const pt_render_config *cfg);

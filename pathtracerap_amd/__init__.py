@@ -88,6 +88,7 @@ EXPORTS = [
                                        _P_F, _P_I, _P_F, _P_I, _P_I]),
     ("pt_scene_export_bvh", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_I, _P_I]),
     ("pt_scene_export_bvh4", ctypes.c_int, [ctypes.c_void_p, _P_F, _P_I]),
+    ("pt_scene_export_bvh4_leaf_base", ctypes.c_int, [ctypes.c_void_p, _P_I]),
     ("pt_renderer_create", ctypes.c_void_p, [ctypes.POINTER(_Cfg)]),
     ("pt_renderer_set_stream", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("pt_renderer_bind_image", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -282,14 +283,18 @@ Scene.export_bvh = _scene_export_bvh
 
 
 def _scene_export_bvh4(self) -> dict:
-    """The 4-wide collapse of the BLAS (Bvh4Node: 32 words per node) and each
-    mesh's 4-wide root (-1: traced with the binary nodes)."""
+    """The 4-wide collapse of the BLAS (Bvh4Node: 32 words per node), each
+    mesh's 4-wide root (-1: none; the 4-wide traces then refuse the scene) and
+    each mesh's first leaf record (`leaf_base`: a leaf link's `first` is
+    relative to it)."""
     n = self.counts()
     roots = np.zeros(max(n["nmesh"], 1), np.int32)
     cnt = _err(lib().pt_scene_export_bvh4(self._h, None, _ip(roots)), "export_bvh4")
     nodes = np.zeros((max(cnt, 1), 32), np.float32)
     _err(lib().pt_scene_export_bvh4(self._h, _fp(nodes), _ip(roots)), "export_bvh4")
-    return dict(nodes=nodes[:cnt], roots=roots[:n["nmesh"]])
+    base = np.zeros(max(n["nmesh"], 1), np.int32)
+    _err(lib().pt_scene_export_bvh4_leaf_base(self._h, _ip(base)), "export_bvh4_leaf_base")
+    return dict(nodes=nodes[:cnt], roots=roots[:n["nmesh"]], leaf_base=base[:n["nmesh"]])
 
 
 Scene.export_bvh4 = _scene_export_bvh4

@@ -279,19 +279,28 @@ int Scene::relayoutPairs(int n0, int root) {
 
 // 4-wide collapse (Bvh4Node): each 4-wide node takes a binary node's children,
 // replacing every inner child by that child's own two children, so it holds
-// 2..4 slots; inner slots become 4-wide nodes in turn (depth-first, a node's
-// inner children next to each other).  Boxes are copied bit for bit.  A mesh
-// whose leaves do not fit the traversal stack's leaf encoding (more than
-// kMaxLeafCount4 triangles, or a first index >= 2^kLeafCountShift) gets no
-// 4-wide BLAS (root -1) and k_trace_gf's binary node steps trace it.
+// 2..4 slots; inner slots become 4-wide nodes in turn, breadth-first (a node's
+// inner children next to each other; a mesh's top levels are its first nodes).
+// PT_BVH4_ORDER=1 renumbers each mesh's nodes depth-first instead (pre-order,
+// children in slot order: a subtree is one contiguous range; layout experiments).
+// Boxes are copied bit for bit.  A leaf's
+// stack entry holds its first record relative to the mesh's first leaf record
+// (mesh_leaf_base, ModelRec::leaf_base, added back by the traces), so the
+// encoding's 2^kLeafCountShift limit is per mesh, not per scene.  A mesh whose
+// leaves still do not fit it (a leaf of more than kMaxLeafCount4 triangles, or
+// 2^kLeafCountShift leaf records or more in one mesh), or whose nodes would pass
+// 2^27 in the scene, gets no 4-wide BLAS (root -1): every BLAS path walks the
+// 4-wide nodes and there is no binary fallback, so Renderer::allocateOnGPU then
+// refuses the scene for them (grid mode, which needs no BLAS, still runs).
 void Scene::buildBvh4() {
     // PT_BVH4_OPEN=0: open the first inner slot instead of the largest (build experiments)
-    static const bool kOpenLargest = [] {
-        const char* e = std::getenv("PT_BVH4_OPEN");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const char* eo = std::getenv("PT_BVH4_OPEN");
+    const bool kOpenLargest = !(eo && std::atoi(eo) == 0);
+    const char* ed = std::getenv("PT_BVH4_ORDER");
+    const bool kDepthFirst = ed && std::atoi(ed) == 1;
     bvh4_nodes.clear();
     mesh_bvh4_root.assign(meshes.size(), -1);
+    mesh_leaf_base.assign(meshes.size(), 0);
     if (bvh_nodes.empty()) return;
     struct Slot { float lo[3], hi[3]; int link, count; };
     auto child = [&](const BvhNode& nd, int c) {
@@ -309,6 +318,21 @@ void Scene::buildBvh4() {
         if (root < 0) continue;
         const size_t n0 = bvh4_nodes.size();
         bool fits = true;
+        // the mesh's first leaf record: its leaf entries are stored relative to it
+        long long base = -1;
+        {
+            std::vector<int> st{root};
+            while (!st.empty()) {
+                const BvhNode nd = bvh_nodes[st.back()];
+                st.pop_back();
+                for (int c = 0; c < 2; c++) {
+                    const int cnt = c ? nd.count1 : nd.count0, lk = c ? nd.link1 : nd.link0;
+                    if (cnt == 0) st.push_back(lk);
+                    else if (cnt > 0 && (base < 0 || lk < base)) base = lk;
+                }
+            }
+        }
+        if (base < 0) base = 0;
         // make(b): the 4-wide node for binary node b; returns its index
         std::vector<std::pair<int, int>> work;   // (binary node, 4-wide index) still to fill
         auto alloc = [&](int b) {
@@ -347,11 +371,16 @@ void Scene::buildBvh4() {
             for (int c = 0; c < 4; c++) {
                 Slot s;
                 if (c < ns) s = slots[c];
-                else {   // an empty slot: an inverted infinite box, which every slab test misses
+                else s.count = -1;
+                if (s.count < 0) {   // an empty slot (past the children, or an empty binary child, as in a
+                                     // 1-triangle mesh): an inverted infinite box, which every slab test misses
                     for (int k = 0; k < 3; k++) { s.lo[k] = INFINITY; s.hi[k] = -INFINITY; }
                     s.link = -1; s.count = -1;
                 }
-                if (s.count > 0 && (s.count > kMaxLeafCount4 || s.link >= (1 << kLeafCountShift))) fits = false;
+                if (s.count > 0) {
+                    s.link -= (int)base;   // mesh-relative (ModelRec::leaf_base)
+                    if (s.count > kMaxLeafCount4 || s.link < 0 || s.link >= (1 << kLeafCountShift)) fits = false;
+                }
                 out.lox[c] = s.lo[0]; out.loy[c] = s.lo[1]; out.loz[c] = s.lo[2];
                 out.hix[c] = s.hi[0]; out.hiy[c] = s.hi[1]; out.hiz[c] = s.hi[2];
                 out.count[c] = s.count;
@@ -362,8 +391,32 @@ void Scene::buildBvh4() {
             }
             bvh4_nodes[id] = out;
         }
+        // node << 4 | slot mask: the one-lane traversal's stack entries (bvh4_traverse)
+        if (bvh4_nodes.size() >= (size_t)1 << 27) fits = false;
+        if (fits && kDepthFirst) {   // renumber [n0, end) in depth-first pre-order
+            const size_t n1 = bvh4_nodes.size();
+            std::vector<int> nid(n1 - n0, -1);
+            std::vector<int> st{r4};
+            int next = (int)n0;
+            while (!st.empty()) {
+                const int b = st.back();
+                st.pop_back();
+                nid[b - n0] = next++;
+                for (int c = 3; c >= 0; c--)
+                    if (bvh4_nodes[b].count[c] == 0) st.push_back(bvh4_nodes[b].link[c]);
+            }
+            std::vector<Bvh4Node> out(n1 - n0);
+            for (size_t i = n0; i < n1; i++) {
+                Bvh4Node nd = bvh4_nodes[i];
+                for (int c = 0; c < 4; c++)
+                    if (nd.count[c] == 0) nd.link[c] = nid[nd.link[c] - n0];
+                out[nid[i - n0] - n0] = nd;
+            }
+            std::copy(out.begin(), out.end(), bvh4_nodes.begin() + n0);
+        }
         if (fits) {
             mesh_bvh4_root[m] = r4;
+            mesh_leaf_base[m] = (int)base;
         } else {
             bvh4_nodes.resize(n0);
         }

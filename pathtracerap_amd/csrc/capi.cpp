@@ -202,6 +202,14 @@ int pt_scene_export_bvh4(const pt_scene* s, float* nodes, int* roots) {
     return (int)S.bvh4_nodes.size();
 }
 
+int pt_scene_export_bvh4_leaf_base(const pt_scene* s, int* bases) {
+    if (!s) return set_err("null scene");
+    const pt::Scene& S = s->s;
+    if (bases)
+        for (size_t i = 0; i < S.meshes.size(); i++) bases[i] = S.mesh_leaf_base.empty() ? 0 : S.mesh_leaf_base[i];
+    return (int)S.meshes.size();
+}
+
 pt_renderer* pt_renderer_create(const pt_render_config* c) {
     if (!c) { set_err("null config"); return nullptr; }
     if (c->accel != PT_ACCEL_GRID && c->accel != PT_ACCEL_BVH && c->accel != PT_ACCEL_GRID_FAST) {

@@ -39,12 +39,12 @@ struct ModelRec {
     float bbox[6];        // mesh bounding box (model space) min3 max3
     float vw[3];          // grid voxel widths
     int vox_start;        // grid->voxelIndices.start_index
-    int mesh;
+    int leaf_base;        // the mesh's first leaf record (bvh_tri_order entry): 4-wide leaf entries are relative to it
     int tri_start, tri_end;
     int bvh_root;         // index of the mesh's BLAS root node
     float wbox[6];        // conservative world-space AABB of everything the instance can hit
     float reach;          // R: max over triangles of the (tolerance-grown) voxel-box diameter, model units
-    int bvh4_root;        // index of the mesh's 4-wide BLAS root (Bvh4Node), -1: trace the binary one
+    int bvh4_root;        // index of the mesh's 4-wide BLAS root (Bvh4Node), -1: none (the 4-wide traces refuse it)
     float wdelta;         // tier-1 window: the walk is exact up to t_min + wdelta
     float ivw[3];         // 1 / vw (rounded; walk certificate only, used with margins)
     float cslack[3];      // walk certificate: position slack per axis (DDA +EPSILON shift + rounding)
@@ -74,8 +74,8 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
 // empty (box lo = +inf, hi = -inf: the node steps' near / far slab test misses
 // it by itself, so they never load count), 0 = inner (link = Bvh4Node index), > 0 = leaf, whose link is already
 // the traversal stack's leaf entry (1 << 31) | count << kLeafCountShift | first
-// (first = its first bvh_tri_order entry), so a node step pushes links as they
-// are.  The same boxes as the binary nodes: only the number of fetches per
+// (first = its first bvh_tri_order entry minus the mesh's ModelRec::leaf_base),
+// so a node step pushes links as they are.  The same boxes as the binary nodes: only the number of fetches per
 // traversal changes, never the set of triangles tested.
 struct Bvh4Node {
     float lox[4], loy[4], loz[4];
@@ -86,7 +86,7 @@ struct Bvh4Node {
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node layout");
 // Leaf children pushed on k_trace_gf's 4-wide traversal stack are encoded as
 // (1 << 31) | (count << kLeafCountShift) | first: count <= kMaxLeafCount4,
-// first < 2^kLeafCountShift (Scene::buildBvh4 checks both).
+// first (mesh-relative) < 2^kLeafCountShift (Scene::buildBvh4 checks both).
 constexpr int kLeafCountShift = 26;
 constexpr int kMaxLeafCount4 = 31;
 

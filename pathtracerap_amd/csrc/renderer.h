@@ -44,10 +44,9 @@ struct KParams {
     const float4* tri_normal;   // 1 float4 per triangle
     const int2* voxels;         // (start, end)
     const int* per_voxel;
-    const BvhNode* bvh;
-    const Bvh4Node* bvh4;       // the same BLAS 4-wide (k_trace_gf node steps; nullptr when the scene has none)
-    const int* bvh_tri;
+    const Bvh4Node* bvh4;       // the BLAS, 4-wide: every BLAS path walks it (nullptr when the scene has none)
     const float4* bvh_tri_geom; // leaf-ordered triangle records, v0.w = triangle index
+    int top_root[2], top_n[2];  // PT_LDS_TOP builds: the two largest meshes' 4-wide roots, nodes staged (<= kLdsTop)
     int* spill;                 // traversal-stack spill beyond the LDS entries, lane-minor
     int spill_stride;           // lanes in the spill layout
     // frame
@@ -93,6 +92,13 @@ struct KParams {
                                         // hands nothing on.  Record buffers alternate between levels
     int drain_dump;                     // hand a wave's rays on once the pool is exhausted and <= this many
                                         // lanes still trace (0: off; PT_DRAIN_DUMP overrides)
+    int drain_dump_tail;                // the same for a tail launch that hands on again (PT_DRAIN_DUMP_TAIL)
+    int tail_rpl;                       // tail launches: waves beyond ceil(records / (64 * tail_rpl)) exit at
+                                        // once, so each lane resumes about tail_rpl records (PT_TAIL_RPL; 1 =
+                                        // one wave per 64 records)
+    int tail_refill;                    // a tail wave claims more records once this many lanes are idle
+    int defer_launch;                   // 0: k_trace_deferred is not launched (PT_DEFER_LAUNCH=0, timing
+                                        // experiments); k_scan then counts a trace fault if any ray was deferred
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,
                                         // counted in segments[kTraceFaultCounter]); PT_TRACE_ITER_CAP overrides
 };

@@ -226,78 +226,106 @@ __device__ __forceinline__ void node_slab(const float* lo, const float* hi, f3 o
     tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
 }
 
-// One node visit of the closest-hit BLAS traversal: test both child boxes,
-// run the triangle tests of hit leaf children, then descend (pushing the far
-// child) or pop.  Returns true when the traversal has finished.  Shared by the
-// per-ray loop (bvh_closest) and the persistent trace kernel (k_trace_bvh).
-template <int STRIDE>
-__device__ __forceinline__ bool bvh_step(const KParams& p, f3 o, f3 d, f3 inv, int& cur, int& sp,
-                                         int* __restrict__ stack, float& best, int& best_tri, bool& any,
-                                         int& n_tris) {
-    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-    const float4 q0 = nodes[4 * cur + 0];
-    const float4 q1 = nodes[4 * cur + 1];
-    const float4 q2 = nodes[4 * cur + 2];
-    const float4 q3 = nodes[4 * cur + 3];
-    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-    const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-    const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-    const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-    float tn0, tf0, tn1, tf1;
-    node_slab(lo0, hi0, o, inv, tn0, tf0);
-    node_slab(lo1, hi1, o, inv, tn1, tf1);
-    bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= best);
-    bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= best);
+// One-lane traversal of a mesh's 4-wide BLAS (Bvh4Node), for the per-ray paths:
+// k_primary, k_trace_deferred, the fused bounce, k_intersect_rays and
+// k_certify_check (the persistent traces have their own phase-scheduled node
+// steps).  A visit tests the slots of `todo` with node_slab's values against
+// bound() (the same fma entries / exits as every other node test), runs the
+// triangles of hit leaf children at once (leaf(first, count), first absolute:
+// ModelRec::leaf_base + the link's mesh-relative first), and descends into the
+// nearest hit inner child.  Its other hit inner children stay on the stack as
+// ONE entry, node << 4 | their slot mask, re-tested against the bound when
+// popped, so the stack holds at most one entry per level of the path (<= the
+// binary depth cap, kMaxBvhDepth + 1 nodes, < kStack) and needs no spill area.
+// Empty slots (count -1) are skipped; the traversal visits every node a binary
+// traversal with the same pruning rule visits, so the triangles tested are a
+// superset of those the bound requires.  leaf() returns false to abort (hit-set
+// overflow); the function then returns false.
+template <int STRIDE, typename Leaf, typename Bound>
+__device__ __forceinline__ bool bvh4_traverse(const KParams& p, const ModelRec& M, f3 o, f3 ninv,
+                                              int* __restrict__ stack, Leaf&& leaf, Bound&& bound, unsigned& nvis) {
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh4);
+    const f3 oi = o * ninv;
+    int cur = M.bvh4_root, sp = 0;
+    if (cur < 0) return true;                        // a mesh without triangles: nothing to traverse
+    unsigned todo = 0xFu;
+    for (;;) {
+        nvis++;
+        const float4* n4 = nodes + 8 * (size_t)cur;
+        const float4 LX = n4[0], LY = n4[1], LZ = n4[2], HX = n4[3], HY = n4[4], HZ = n4[5], LK = n4[6], CN = n4[7];
+        const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, ly[4] = {LY.x, LY.y, LY.z, LY.w}, lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w};
+        const float hx[4] = {HX.x, HX.y, HX.z, HX.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+        const int lk[4] = {__float_as_int(LK.x), __float_as_int(LK.y), __float_as_int(LK.z), __float_as_int(LK.w)};
+        const int cn[4] = {__float_as_int(CN.x), __float_as_int(CN.y), __float_as_int(CN.z), __float_as_int(CN.w)};
+        const float bd = bound();
+        int next = -1;
+        float next_t = 0.0f;
+        unsigned rest = 0;
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
-        const bool hc = c == 0 ? h0 : h1;
-        const int cc = c == 0 ? cnt0 : cnt1;
-        const int lc = c == 0 ? link0 : link1;
-        if (hc && cc > 0) {
-            for (int i = lc; i < lc + cc; i++) {
-                const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
-                const int it = __float_as_int(A.w);
-                float t;
-                n_tris++;
-                if (tri_test_rec(A, B, C, o, d, t)) {
-                    any = true;
-                    if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
-                }
+        for (int c = 0; c < 4; c++) {
+            if (!((todo >> c) & 1u) || cn[c] < 0) continue;
+            const float a0 = __builtin_fmaf(lx[c], ninv.x, -oi.x), b0 = __builtin_fmaf(hx[c], ninv.x, -oi.x);
+            const float a1 = __builtin_fmaf(ly[c], ninv.y, -oi.y), b1 = __builtin_fmaf(hy[c], ninv.y, -oi.y);
+            const float a2 = __builtin_fmaf(lz[c], ninv.z, -oi.z), b2 = __builtin_fmaf(hz[c], ninv.z, -oi.z);
+            const float tn = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fminf(a2, b2));
+            const float tf = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fmaxf(a2, b2));
+            if (!((tn <= tf) & (tf >= -kEps) & (tn <= bd))) continue;
+            if (cn[c] > 0) {                         // a leaf: its link is the stack's leaf entry
+                if (!leaf(M.leaf_base + (lk[c] & ((1 << kLeafCountShift) - 1)), cn[c])) return false;
+                continue;
+            }
+            if (next < 0 || tn < next_t) {
+                if (next >= 0) rest |= 1u << next;
+                next = c;
+                next_t = tn;
+            } else {
+                rest |= 1u << c;
             }
         }
-    }
-    h0 = h0 && cnt0 == 0;
-    h1 = h1 && cnt1 == 0;
-    if (h0 && h1) {
-        const bool first0 = tn0 <= tn1;
-        stack[sp * STRIDE] = first0 ? link1 : link0;
-        sp++;
-        cur = first0 ? link0 : link1;
-    } else if (h0) {
-        cur = link0;
-    } else if (h1) {
-        cur = link1;
-    } else {
+        if (rest) {
+            if (sp >= kStack) {                      // cannot happen (one entry per level); reported as a fault
+                atomicAdd(p.segments + kTraceFaultCounter, 1ull);
+                return true;
+            }
+            stack[sp * STRIDE] = (cur << 4) | (int)rest;
+            sp++;
+        }
+        if (next >= 0) {
+            cur = lk[next];
+            todo = 0xFu;
+            continue;
+        }
         if (sp == 0) return true;
         sp--;
-        cur = stack[sp * STRIDE];
+        const int e = stack[sp * STRIDE];
+        cur = e >> 4;
+        todo = (unsigned)e & 0xFu;
     }
-    return false;
 }
 
 // Exact closest hit over the mesh's triangles via its BLAS.  Matches the
-// brute-force scan in triangle-index order: (t, index) lexicographic minimum.
+// brute-force scan in triangle-index order: (t, index) lexicographic minimum
+// (a node is pruned only when entered beyond the best t, so a tie with a
+// smaller index is still reached).
 template <int STRIDE>
-__device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, float& best, int& best_tri,
+__device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 ninv, float& best, int& best_tri,
                             int* __restrict__ stack) {
     bool any = false;
-    int sp = 0;
-    int cur = M.bvh_root;
-    int n_nodes = 0, n_tris = 0;     // PT_DEBUG_ABLATE & 8 statistics
-    for (;;) {
-        n_nodes++;
-        if (bvh_step<STRIDE>(p, o, d, inv, cur, sp, stack, best, best_tri, any, n_tris)) break;
-    }
+    unsigned n_nodes = 0, n_tris = 0;   // PT_DEBUG_ABLATE & 8 statistics
+    auto leaf = [&](int first, int count) {
+        for (int i = first; i < first + count; i++) {
+            const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
+            const int it = __float_as_int(A.w);
+            float t;
+            n_tris++;
+            if (tri_test_rec(A, B, C, o, d, t)) {
+                any = true;
+                if (t < best || (t == best && it < best_tri)) { best = t; best_tri = it; }
+            }
+        }
+        return true;
+    };
+    bvh4_traverse<STRIDE>(p, M, o, ninv, stack, leaf, [&] { return best; }, n_nodes);
     if (PT_TRACE_STATS && (p.debug & 8)) {
         atomicAdd(p.segments + 4 + kMaxBounceCounters, (unsigned long long)n_nodes);
         atomicAdd(p.segments + 5 + kMaxBounceCounters, (unsigned long long)n_tris);
@@ -311,86 +339,49 @@ constexpr int kHitCapPool = 64;      // global pool block (members); overflow ->
 
 // BLAS traversal collecting hit-set members: triangles the reference test
 // accepts, as (t bits, index, packed voxel box lo, hi) in the lane's LDS slots
-// hs[i * STRIDE].  BOUNDED: only members with t <= t_min + 2R are required
-// (nodes entered beyond that are pruned; extra members are harmless).
+// hs[i * STRIDE].  BOUNDED: only members with t <= t_min + margin are required
+// (nodes entered beyond that are pruned; extra members are harmless: t_min only
+// falls, so a required member's node is never pruned, in any visit order).
 // Returns the count (-1 on overflow); *tmin_out = smallest t accepted.
 template <int STRIDE, bool BOUNDED, int HSTRIDE = STRIDE, int CAP = kHitCap>
-__device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 inv, int* __restrict__ stack,
+__device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 ninv, int* __restrict__ stack,
                            int4* __restrict__ hs, float* tmin_out, float margin) {
     int nh = 0;
     float tmin = kFMax;
-    int sp = 0;
-    int cur = M.bvh_root;
-    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
     unsigned nvis = 0;
-    for (;;) {
-        nvis++;
-        const float4 q0 = nodes[4 * cur + 0];
-        const float4 q1 = nodes[4 * cur + 1];
-        const float4 q2 = nodes[4 * cur + 2];
-        const float4 q3 = nodes[4 * cur + 3];
-        const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-        const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-        const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-        const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-        float tn0, tf0, tn1, tf1;
-        node_slab(lo0, hi0, o, inv, tn0, tf0);
-        node_slab(lo1, hi1, o, inv, tn1, tf1);
-        const float bound = BOUNDED ? tmin + margin : 3.0e38f;
-        bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= bound);
-        bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= bound);
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const bool hc = c == 0 ? h0 : h1;
-            const int cc = c == 0 ? cnt0 : cnt1;
-            const int lc = c == 0 ? link0 : link1;
-            if (hc && cc > 0) {
-                for (int i = lc; i < lc + cc; i++) {
-                    const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
-                    float t;
-                    if (!tri_test_rec(A, B, C, o, d, t)) continue;
-                    if (BOUNDED) {
-                        if (t < tmin) tmin = t;
-                        if (t > tmin + margin) continue;          // not required (NaN is kept)
-                        if (nh == CAP) {                           // drop members now beyond the bound
-                            int w = 0;
-                            for (int q = 0; q < nh; q++) {
-                                const int4 e = hs[q * HSTRIDE];
-                                if (!(__int_as_float(e.x) > tmin + margin)) hs[(w++) * HSTRIDE] = e;
-                            }
-                            nh = w;
-                        }
-                    } else if (t < tmin) {
-                        tmin = t;
+    auto leaf = [&](int first, int count) {
+        for (int i = first; i < first + count; i++) {
+            const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
+            float t;
+            if (!tri_test_rec(A, B, C, o, d, t)) continue;
+            if (BOUNDED) {
+                if (t < tmin) tmin = t;
+                if (t > tmin + margin) continue;          // not required (NaN is kept)
+                if (nh == CAP) {                           // drop members now beyond the bound
+                    int w = 0;
+                    for (int q = 0; q < nh; q++) {
+                        const int4 e = hs[q * HSTRIDE];
+                        if (!(__int_as_float(e.x) > tmin + margin)) hs[(w++) * HSTRIDE] = e;
                     }
-                    if (nh == CAP) return -1;
-                    hs[nh * HSTRIDE] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
-                                                 __float_as_int(C.w));
-                    nh++;
+                    nh = w;
                 }
+            } else if (t < tmin) {
+                tmin = t;
             }
+            if (nh == CAP) return false;
+            hs[nh * HSTRIDE] = make_int4(__float_as_int(t), __float_as_int(A.w), __float_as_int(B.w),
+                                         __float_as_int(C.w));
+            nh++;
         }
-        if (cnt0 > 0) h0 = false;
-        if (cnt1 > 0) h1 = false;
-        if (h0 && h1) {
-            const bool first0 = tn0 <= tn1;                         // near child first tightens the bound
-            stack[sp * STRIDE] = first0 ? link1 : link0;
-            sp++;
-            cur = first0 ? link0 : link1;
-        } else if (h0) {
-            cur = link0;
-        } else if (h1) {
-            cur = link1;
-        } else {
-            if (sp == 0) break;
-            sp--;
-            cur = stack[sp * STRIDE];
-        }
-    }
+        return true;
+    };
+    const bool ok = bvh4_traverse<STRIDE>(p, M, o, ninv, stack, leaf,
+                                          [&] { return BOUNDED ? tmin + margin : 3.0e38f; }, nvis);
     if (PT_TRACE_STATS && (p.debug & 4)) {          // collection statistics: node visits, collections
         atomicAdd(p.segments + 22 + kMaxBounceCounters, (unsigned long long)nvis);
         atomicAdd(p.segments + 23 + kMaxBounceCounters, 1ull);
     }
+    if (!ok) return -1;
     *tmin_out = tmin;
     return nh;
 }
@@ -1301,9 +1292,6 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
 #ifndef PT_BVH_NODE_STEP
 #define PT_BVH_NODE_STEP 4    // k_trace_bvh: node visits per node step (as PT_NODE_STEP)
 #endif
-#ifndef PT_BVH_BVH4
-#define PT_BVH_BVH4 1         // k_trace_bvh: node steps over the 4-wide BLAS (stack spills past kStack); 0: binary
-#endif
 #ifndef PT_BVH_SEL_MASK
 #define PT_BVH_SEL_MASK 1     // k_trace_bvh: PT_SEL_MASK's candidate mask for the main launch's select steps
 #endif
@@ -1367,10 +1355,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModels) : 1;
     __shared__ ModelRec s_models[kModelsHere];
     int* stack = s_stack + threadIdx.x;
-    // the binary BLAS's depth cap keeps its whole traversal stack in LDS; the 4-wide traversal
-    // (up to three pushes per node) spills past kStack entries to this lane's global area
-    constexpr bool kBvh4 = PT_BVH_BVH4 != 0;
-    static_assert(!kBvh4 || 3 * (kMaxBvhDepth + 1) + 1 <= kStack + kSpillEntries,
+    // the 4-wide traversal (up to three pushes per node) spills past kStack entries to this
+    // lane's global area
+    static_assert(3 * (kMaxBvhDepth + 1) + 1 <= kStack + kSpillEntries,
                   "k_trace_bvh's 4-wide traversal stack (LDS + spill) too small");
     int sbase = (int)(blockIdx.x * BS + threadIdx.x);   // this lane's spill area (a resumed ray brings its own)
     int* spill = p.spill + sbase;
@@ -1381,6 +1368,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     const bool may_dump = level < p.drain_levels;
     const int ncont = TAIL ? p.cont_count[level - 1] : 0;
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
+    if (TAIL && p.tail_rpl > 1 && (int)blockIdx.x >= (ncont + BS * p.tail_rpl - 1) / (BS * p.tail_rpl)) return;
     // Sparse bounces: a main launch whose rays come to fewer than trace_rpl per lane runs only
     // as many waves as give each lane that many (the rest exit at once), so fewer waves pay
     // the drain -- the wait on each wave's slowest rays once the claim counter runs out.
@@ -1412,6 +1400,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 0), ninv = mk3(0, 0, 0);
     int cur = 0, sp = 0, best_tri = -1;
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0;    // pending leaves: [lf_i, lf_e) then [lf2_i, lf2_e)
+    int lbase = 0;                                  // ModelRec::leaf_base of the model being traced
     int lf_next = -1;                               // then node lf_next (-1: pop the stack)
     float best = kFMax;
     bool any = false, exhausted = false;
@@ -1425,7 +1414,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        if (idle && !exhausted && (busy == 0 || __popcll(idle) >= (TAIL ? p.tail_refill : p.trace_refill))) {
             if (TAIL) {                                     // resume continuation records
                 const int cnt = __popcll(idle);
                 const int leader = __ffsll((long long)idle) - 1;
@@ -1447,7 +1436,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         cur = C[kCCur * cs]; sp = C[kCSp * cs];
                         lf_i = C[kCLfI * cs]; lf_e = C[kCLfE * cs]; lf2_i = C[kCLf2I * cs]; lf2_e = C[kCLf2E * cs];
                         lf_next = C[kCLfNext * cs];
-                        if (kBvh4) { sbase = C[kCSpill * cs]; spill = p.spill + sbase; }
+                        sbase = C[kCSpill * cs]; spill = p.spill + sbase;
                         best = __int_as_float(C[kCX * cs]); best_tri = C[(kCX + 1) * cs]; any = C[(kCX + 2) * cs] != 0;
 #pragma unroll 1
                         for (int q = 0; q < kStack; q++) stack[q * BS] = C[(kCX + 3 + q) * cs];
@@ -1455,6 +1444,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         dlen = sqrtf(dot(dw, dw));
                         if (state != 1) {                   // inside model im: its model-space ray, as selected
                             const ModelRec& M = models[im];
+                            lbase = M.leaf_base;
                             o = xform12(M.w2m, ow, 1.0f);
                             d = normalize(xform12(M.w2m, dw, 0.0f));
                             const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -1511,7 +1501,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             if (c1 * 4 > cm * PT_BVH_SEL_W) phase = 1;
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
-        if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
+        {
+            const int dd = TAIL ? p.drain_dump_tail : p.drain_dump;
+            if (may_dump && exhausted && dd > 0 && __popcll(__ballot(state != 3)) <= dd) phase = 16;
+        }
         phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
@@ -1577,11 +1570,13 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
                     if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;
                 } else if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (M.bvh4_root < 0) continue;              // a mesh without triangles: no hit, no BLAS
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
                 ninv = node_inv(inv);
-                cur = kBvh4 ? M.bvh4_root : M.bvh_root;
+                cur = M.bvh4_root;
+                lbase = M.leaf_base;
                 sp = 0;
                 best = kFMax;
                 best_tri = -1;
@@ -1611,36 +1606,21 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 }
             }
             lf_i = min(lf_i + PT_LEAF_STEP, lf_e);
-            if (kBvh4) {
-                // end of the leaf: the next stack entry, a leaf (encoded, < 0) or a node
-                const bool end = lf_i == lf_e;
-                const bool pop = end & (sp > 0);
-                model_done = end & (sp == 0);
-                const int top = spop_if<BS, kStack>(pop, stack, spill, p.spill_stride, sp - 1);
-                sp -= pop ? 1 : 0;
-                const bool tleaf = pop & (top < 0);
-                const int first = top & ((1 << kLeafCountShift) - 1);
-                lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
-                lf_i = tleaf ? first : lf_i;
-                cur = (pop & !tleaf) ? top : cur;
-                state = (pop & !tleaf) ? 2 : state;
-            } else {
-                // end of the leaf: second leaf child, `next`, or the stack (selects)
-                const bool end = lf_i == lf_e;
-                const bool second = end & (lf2_i < lf2_e);
-                const bool tonext = end & !second & (lf_next >= 0);
-                const bool pop = end & !second & !tonext & (sp > 0);
-                model_done = end & !second & !tonext & (sp == 0);
-                const int top = stack[max(sp - 1, 0) * BS];
-                lf_i = second ? lf2_i : lf_i;
-                lf_e = second ? lf2_e : lf_e;
-                lf2_i = second ? 0 : lf2_i;
-                lf2_e = second ? 0 : lf2_e;
-                cur = tonext ? lf_next : (pop ? top : cur);
-                state = (tonext | pop) ? 2 : state;
-                sp -= pop ? 1 : 0;
+            {
+            // end of the leaf: the next stack entry, a leaf (encoded, < 0) or a node
+            const bool end = lf_i == lf_e;
+            const bool pop = end & (sp > 0);
+            model_done = end & (sp == 0);
+            const int top = spop_if<BS, kStack>(pop, stack, spill, p.spill_stride, sp - 1);
+            sp -= pop ? 1 : 0;
+            const bool tleaf = pop & (top < 0);
+            const int first = lbase + (top & ((1 << kLeafCountShift) - 1));   // mesh-relative entry
+            lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
+            lf_i = tleaf ? first : lf_i;
+            cur = (pop & !tleaf) ? top : cur;
+            state = (pop & !tleaf) ? 2 : state;
             }
-        } else if (kBvh4 && (phase & 2) && state == 2) {
+        } else if ((phase & 2) && state == 2) {   // 4-wide node steps
 #pragma unroll 1
             for (int ks = 0; ks < PT_BVH_NODE_STEP; ks++) {
                 // 4-wide node visits: every hit child in order of entry, nearest first
@@ -1687,52 +1667,10 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 sp -= pop ? 1 : 0;
                 const int nx = nhit > 0 ? ent[0] : top;
                 const bool leaf = !model_done & (nx < 0);
-                const int first = nx & ((1 << kLeafCountShift) - 1);
+                const int first = lbase + (nx & ((1 << kLeafCountShift) - 1));
                 lf_i = leaf ? first : lf_i;
                 lf_e = leaf ? first + ((nx >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
                 cur = (!model_done & !leaf) ? nx : cur;
-                state = leaf ? 4 : state;
-                if (state != 2 || model_done) break;
-            }
-        } else if ((phase & 2) && state == 2) {
-#pragma unroll 1
-            for (int ks = 0; ks < PT_BVH_NODE_STEP; ks++) {
-                // node visits (lanes still at an inner node go on); hit leaf children become
-                // pending leaves (tested in the order bvh_step tests them)
-                const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-                const float4 q0 = nodes[4 * cur + 0];
-                const float4 q1 = nodes[4 * cur + 1];
-                const float4 q2 = nodes[4 * cur + 2];
-                const float4 q3 = nodes[4 * cur + 3];
-                const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-                const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-                const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-                const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-                float tn0, tf0, tn1, tf1;
-                node_slab(lo0, hi0, o, ninv, tn0, tf0);
-                node_slab(lo1, hi1, o, ninv, tn1, tf1);
-                const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tn0 <= best);
-                const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tn1 <= best);
-                // next node after the leaves: same rule as bvh_step; the decisions as
-                // selects, only the push and the (LDS) stack-top read touch memory
-                const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
-                const bool i0 = h0 & (cnt0 == 0), i1 = h1 & (cnt1 == 0);
-                const bool both = i0 & i1;
-                const bool first0 = tn0 <= tn1;
-                const int next = both ? (first0 ? link0 : link1) : (i0 ? link0 : (i1 ? link1 : -1));
-                if (both) stack[sp * BS] = first0 ? link1 : link0;
-                sp += both ? 1 : 0;
-                const bool leaf = l0 | l1;              // leaf 0, then leaf 1, then `next`
-                const bool pop = !leaf & (next < 0) & (sp > 0);
-                const int top = stack[max(sp - 1, 0) * BS];
-                model_done = !leaf & (next < 0) & (sp == 0);
-                sp -= pop ? 1 : 0;
-                cur = leaf ? cur : (next >= 0 ? next : (pop ? top : cur));
-                lf_i = leaf ? (l0 ? link0 : link1) : lf_i;
-                lf_e = leaf ? lf_i + (l0 ? cnt0 : cnt1) : lf_e;
-                lf2_i = leaf ? ((l0 & l1) ? link1 : 0) : lf2_i;
-                lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
-                lf_next = leaf ? next : lf_next;
                 state = leaf ? 4 : state;
                 if (state != 2 || model_done) break;
             }
@@ -1798,14 +1736,16 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
-#ifndef PT_GF_BVH4
-#define PT_GF_BVH4 1          // k_trace_gf: node steps over the 4-wide BLAS (Bvh4Node); 0: the binary one
+#ifndef PT_LDS_TOP
+#define PT_LDS_TOP 0          // k_trace_gf: top 4-wide nodes per mesh staged in LDS (experiment; 0 = off)
 #endif
-constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP;
-constexpr bool kGfBvh4 = PT_GF_BVH4 != 0;
+#ifndef PT_LDS_TOP_MESHES
+#define PT_LDS_TOP_MESHES 2   // ... of the largest one or two meshes
+#endif
+constexpr int kGfStack = PT_GF_STACK, kGfHitCap = PT_GF_HITCAP, kLdsTop = PT_LDS_TOP, kLdsTopMeshes = PT_LDS_TOP_MESHES;
 // 4-wide traversal: at most 3 pushes per node on a path of at most kMaxBvhDepth + 1 nodes (an unopened
 // slot keeps its binary level, so a 4-wide path can be as long as a binary one)
-static_assert(!kGfBvh4 || 3 * (kMaxBvhDepth + 1) + 1 <= kGfStack + kSpillEntries,
+static_assert(3 * (kMaxBvhDepth + 1) + 1 <= kGfStack + kSpillEntries,
               "k_trace_gf's 4-wide traversal stack (LDS + spill) too small");
 
 // Test hook: the walk certificates against the exact walk on the same hit set.
@@ -1912,6 +1852,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     __shared__ int4 s_hs[kGfHitCap * BS];
     constexpr int kModelsHere = (F & 1) ? ((F & 32) ? kLdsModelsWide : kLdsModelsGf) : 1;
     __shared__ ModelRec s_models[kModelsHere];
+    // PT_LDS_TOP (experiment, default 0): the first kLdsTop 4-wide nodes (breadth-first: the
+    // root, then level 1, ...) of the two largest meshes (KParams::top_root / top_n) in LDS
+    __shared__ float4 s_top[kLdsTop > 0 ? kLdsTopMeshes * kLdsTop * 8 : 1];
     // PT_SEL_MASK: per lane, the models whose world box the ray can reach (gdist aside),
     // found once per ray so later select steps jump to the next candidate
     constexpr bool kSelMask = PT_SEL_MASK && !TAIL && (F & 1);
@@ -1933,6 +1876,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     const int nd = TAIL ? p.cont_count[level - 1] : 0;
     const int ncont = nd + (TAIL && level == 1 ? min(p.cont_count[kDrainLevels], p.cont_wcap) : 0);
     if (TAIL && (int)blockIdx.x * BS >= ncont) return;  // more waves than records (uniform per block)
+    // a tail launch sized to its records: each lane resumes about tail_rpl of them, refilling as
+    // its rays finish, so fewer waves pay the wait on their slowest resumed ray
+    if (TAIL && p.tail_rpl > 1 && (int)blockIdx.x >= (ncont + BS * p.tail_rpl - 1) / (BS * p.tail_rpl)) return;
     // Sparse bounces: a main launch whose rays come to fewer than trace_rpl per lane runs only
     // as many waves as give each lane that many (the rest exit at once), so fewer waves pay
     // the drain -- the wait on each wave's slowest rays once the claim counter runs out.
@@ -1951,6 +1897,14 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         for (int i = threadIdx.x; i < nw; i += BS) dst[i] = src[i];
         __syncthreads();
     }
+    if (kLdsTop > 0) {
+        const float4* nodes4 = reinterpret_cast<const float4*>(p.bvh4);
+        for (int i = threadIdx.x; i < kLdsTopMeshes * kLdsTop * 8; i += BS) {
+            const int m = i / (kLdsTop * 8), k = (i / 8) % kLdsTop;
+            s_top[i] = k < p.top_n[m] ? nodes4[8 * (size_t)(p.top_root[m] + k) + (i & 7)] : make_float4(0, 0, 0, 0);
+        }
+        __syncthreads();
+    }
     const ModelRec* models = lds_models ? s_models : p.models;
     const int n = p.n_live[bounce];
     const int in_buf = (bounce + 1) & 1;
@@ -1966,6 +1920,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
+    int lbase = 0;                                  // ModelRec::leaf_base of the model being traced
     bool exhausted = false;
     unsigned cmask = 0;                            // PT_SEL_MASK: candidate models of the lane's ray
     unsigned long long st_iter = 0, st_node = 0, st_leaf = 0, st_walk = 0, st_sel = 0;   // PT_DEBUG_ABLATE & 16
@@ -1979,7 +1934,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     for (unsigned iters = 0;; iters++) {
         unsigned long long idle = __ballot(state == 0);
         const unsigned long long busy = __ballot(state != 0 && state != 3);
-        if (TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.trace_refill)) {
+        if (TAIL && idle && !exhausted && (busy == 0 || __popcll(idle) >= p.tail_refill)) {
             // resume continuation records
             const int cnt = __popcll(idle);
             const int leader = __ffsll((long long)idle) - 1;
@@ -2018,6 +1973,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                                                C[(kCX + 11 + kGfStack + 4 * q) * cs], C[(kCX + 12 + kGfStack + 4 * q) * cs]);
                     if (state > 1) {                        // inside model im: its model-space ray, as selected
                         const ModelRec& M = models[im];
+                        lbase = M.leaf_base;
                         o = xform12(M.w2m, ow, 1.0f);
                         d = normalize(xform12(M.w2m, dw, 0.0f));
                         const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -2096,7 +2052,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (c1 * 4 > cm * PT_SEL_W) { phase = 1; cm = c1; }
         }
         // drain: at most drain_dump lanes still trace once the pool is exhausted
-        if (may_dump && exhausted && p.drain_dump > 0 && __popcll(__ballot(state != 3)) <= p.drain_dump) phase = 16;
+        {
+            const int dd = TAIL ? p.drain_dump_tail : p.drain_dump;
+            if (may_dump && exhausted && dd > 0 && __popcll(__ballot(state != 3)) <= dd) phase = 16;
+        }
         phase = __builtin_amdgcn_readfirstlane(phase);   // wave-uniform: scalar branches on it
         if (PT_TRACE_STATS && (p.debug & 16)) {       // lane-steps executed per phase, and phase iterations
             st_iter++;
@@ -2150,6 +2109,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
                     if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;
                 } else if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
+                if (M.bvh4_root < 0) continue;              // a mesh without triangles: no hit, no BLAS
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -2167,7 +2127,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 if (PT_TRACE_STATS && (p.debug & 1024)) G = mk3(0, 0, 0);   // timing-only ablation: no growth
                 tier = 0;
                 win = (PT_TRACE_STATS && (p.debug & 256)) ? 0.0f : M.wdelta;   // 256: timing-only ablation
-                cur = kGfBvh4 ? M.bvh4_root : M.bvh_root;
+                cur = M.bvh4_root;
+                lbase = M.leaf_base;
                 sp = 0; nh = 0; tmin = kFMax; pblk = -1;
                 state = 2;
                 break;
@@ -2242,7 +2203,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     }
                 }
             }
-            if (kGfBvh4 && state == 4) {
+            if (state == 4) {
                 lf_i += n_step;
                 // end of the leaf: the next stack entry, a leaf (encoded, < 0) or a node
                 const bool end = lf_i == lf_e;
@@ -2251,36 +2212,40 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
                 sp -= pop ? 1 : 0;
                 const bool tleaf = pop & (top < 0);
-                const int first = top & ((1 << kLeafCountShift) - 1);
+                const int first = lbase + (top & ((1 << kLeafCountShift) - 1));   // mesh-relative entry
                 lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
                 lf_i = tleaf ? first : lf_i;
                 cur = (pop & !tleaf) ? top : cur;
                 state = (pop & !tleaf) ? 2 : state;
-            } else if (state == 4) {
-                lf_i += n_step;                     // with two, the first never ends the list
-                // end of the leaf: second leaf child, `next`, or the stack (selects)
-                const bool end = lf_i == lf_e;
-                const bool second = end & (lf2_i < lf2_e);
-                const bool tonext = end & !second & (lf_next >= 0);
-                const bool pop = end & !second & !tonext & (sp > 0);
-                collected = end & !second & !tonext & (sp == 0);
-                const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
-                lf_i = second ? lf2_i : lf_i;
-                lf_e = second ? lf2_e : lf_e;
-                lf2_i = second ? 0 : lf2_i;
-                lf2_e = second ? 0 : lf2_e;
-                cur = tonext ? lf_next : (pop ? top : cur);
-                state = (tonext | pop) ? 2 : state;
-                sp -= pop ? 1 : 0;
             }
-        } else if (kGfBvh4 && (phase & 2) && state == 2) {   // 4-wide node steps of the collection
+        } else if ((phase & 2) && state == 2) {   // 4-wide node steps of the collection
 #pragma unroll 1
             for (int ks = 0; ks < kNodeSteps; ks++) {
                 // per axis, the slab a child is entered through is fixed by the sign of the slope:
                 // load each axis' near and far planes directly (lo for a positive slope), so the
                 // entries and exits come without min / max, and the voxel-grown entry is one fma
                 const int ox = ninv.x < 0.0f ? 3 : 0, oy = ninv.y < 0.0f ? 3 : 0, oz = ninv.z < 0.0f ? 3 : 0;
+#if PT_LDS_TOP
+                const int rel0_ = cur - p.top_root[0], rel1_ = cur - p.top_root[1];
+                const bool in0_ = (unsigned)rel0_ < (unsigned)p.top_n[0];
+                const bool in1_ = kLdsTopMeshes > 1 && (unsigned)rel1_ < (unsigned)p.top_n[1];
+                float4 NX, NY, NZ, FX, FY, FZ, LKf;
+                if (in0_ | in1_) {
+                    const float4* q_ = s_top + 8 * (in0_ ? rel0_ : kLdsTop + rel1_);
+                    NX = q_[ox]; NY = q_[1 + oy]; NZ = q_[2 + oz];
+                    FX = q_[3 - ox]; FY = q_[4 - oy]; FZ = q_[5 - oz];
+                    LKf = q_[6];
+                } else {
+                    const char* __restrict__ nb_ = reinterpret_cast<const char*>(p.bvh4);
+                    const unsigned nbo_ = (unsigned)cur << 7;
+                    auto ld4_ = [&](int q) { return *reinterpret_cast<const float4*>(nb_ + (nbo_ + 16u * (unsigned)q)); };
+                    NX = ld4_(ox); NY = ld4_(1 + oy); NZ = ld4_(2 + oz);
+                    FX = ld4_(3 - ox); FY = ld4_(4 - oy); FZ = ld4_(5 - oz);
+                    LKf = ld4_(6);
+                }
+#else
                 PT_NODE_LOADS(cur, ox, oy, oz)
+#endif
                 const float pnx[4] = {NX.x, NX.y, NX.z, NX.w}, pny[4] = {NY.x, NY.y, NY.z, NY.w};
                 const float pnz[4] = {NZ.x, NZ.y, NZ.z, NZ.w}, pfx[4] = {FX.x, FX.y, FX.z, FX.w};
                 const float pfy[4] = {FY.x, FY.y, FY.z, FY.w}, pfz[4] = {FZ.x, FZ.y, FZ.z, FZ.w};
@@ -2338,59 +2303,12 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 sp -= pop ? 1 : 0;
                 const int nx = nhit > 0 ? ent[0] : top;       // the entry to go on with (when not collected)
                 const bool leaf = !collected & (nx < 0);
-                const int first = nx & ((1 << kLeafCountShift) - 1);
+                const int first = lbase + (nx & ((1 << kLeafCountShift) - 1));
                 lf_i = leaf ? first : lf_i;
                 lf_e = leaf ? first + ((nx >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
                 cur = (!collected & !leaf) ? nx : cur;
                 state = leaf ? 4 : state;
                 if (state != 2 || collected) break;    // a leaf reached, or the collection done
-                if (kNodeMinLanes > 0 && __popcll(__ballot(state == 2 && !collected)) < kNodeMinLanes) break;
-            }
-        } else if ((phase & 2) && state == 2) {         // PT_NODE_STEP nodes of the collection (window t_min + win)
-#pragma unroll 1
-            for (int ks = 0; ks < kNodeSteps; ks++) {
-                const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh);
-                const float4 q0 = nodes[4 * cur + 0];
-                const float4 q1 = nodes[4 * cur + 1];
-                const float4 q2 = nodes[4 * cur + 2];
-                const float4 q3 = nodes[4 * cur + 3];
-                const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q1.x, q1.y, q1.z};
-                const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q3.x, q3.y, q3.z};
-                const int link0 = __float_as_int(q0.w), link1 = __float_as_int(q1.w);
-                const int cnt0 = __float_as_int(q2.w), cnt1 = __float_as_int(q3.w);
-                float tn0, tf0, tn1, tf1, tx0, tx1;
-                node_slab_g(lo0, hi0, o, ninv, G, tn0, tf0, tx0);
-                node_slab_g(lo1, hi1, o, ninv, G, tn1, tf1, tx1);
-                const float X = tmin + win;
-                const float bound = X + gf_slack(X, t_box);
-                // non-short-circuit: both children's slabs in one basic block (a branch on
-                // cnt >= 0 moved the float work into its own block, where every min/max
-                // operand was re-canonicalised)
-                const bool h0 = (cnt0 >= 0) & (tn0 <= tf0) & (tf0 >= -kEps) & (tx0 <= bound);
-                const bool h1 = (cnt1 >= 0) & (tn1 <= tf1) & (tf1 >= -kEps) & (tx1 <= bound);
-                // the step's decisions as selects; only the push and the pop touch memory
-                // (the traces are issue-bound: every divergent branch costs scalar exec-mask work)
-                const bool l0 = h0 & (cnt0 > 0), l1 = h1 & (cnt1 > 0);
-                const bool i0 = h0 & (cnt0 == 0), i1 = h1 & (cnt1 == 0);
-                const bool both = i0 & i1;
-                const bool first0 = tn0 <= tn1;             // near child first tightens the bound
-                const int next = both ? (first0 ? link0 : link1) : (i0 ? link0 : (i1 ? link1 : -1));
-                if (both) spush_t<BS, kGfStack>(stack, spill, p.spill_stride, sp, first0 ? link1 : link0);
-                sp += both ? 1 : 0;
-                const bool leaf = l0 | l1;                  // leaf 0, then leaf 1, then `next`
-                const bool pop = !leaf & (next < 0) & (sp > 0);
-                const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
-                collected = !leaf & (next < 0) & (sp == 0);
-                sp -= pop ? 1 : 0;
-                cur = leaf ? cur : (next >= 0 ? next : (pop ? top : cur));
-                lf_i = leaf ? (l0 ? link0 : link1) : lf_i;
-                lf_e = leaf ? lf_i + (l0 ? cnt0 : cnt1) : lf_e;
-                lf2_i = leaf ? ((l0 & l1) ? link1 : 0) : lf2_i;
-                lf2_e = leaf ? ((l0 & l1) ? link1 + cnt1 : 0) : lf2_e;
-                lf_next = leaf ? next : lf_next;
-                state = leaf ? 4 : state;
-                if (state != 2 || collected) break;    // a leaf reached, or the collection done
-                // PT_NODE_MINLANES: the whole wave leaves the step once few lanes are still at a node
                 if (kNodeMinLanes > 0 && __popcll(__ballot(state == 2 && !collected)) < kNodeMinLanes) break;
             }
         }
@@ -2406,7 +2324,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 const ModelRec& M = models[im];
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = kGfBvh4 ? M.bvh4_root : M.bvh_root;
+                cur = M.bvh4_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2465,7 +2383,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             } else {                                    // not provably exact: next tier's collection
                 tier++;
                 win = tier == 1 ? 2.0f * M.reach : 3.0e38f;
-                cur = kGfBvh4 ? M.bvh4_root : M.bvh_root;
+                cur = M.bvh4_root;
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
@@ -2731,6 +2649,8 @@ __global__ __launch_bounds__(kScanWG) void k_scan(KParams p, int bounce) {
         }
         *p.hs_pool_next = 0;       // the next bounce starts with an empty hit-set pool
         *p.trace_next = 0;         // and an unclaimed persistent-trace counter
+        // (a skipped k_trace_deferred launch left deferred rays untraced: their hit records are stale)
+        if (!p.defer_launch && bounce > 0 && *p.defer_count > 0) atomicAdd(p.segments + kTraceFaultCounter, 1ull);
         *p.defer_count = 0;        // and no deferred grid_fast rays
         for (int l = 0; l < kDrainLevels; l++) {   // and no drain continuations or walk hand-ons
             p.cont_count[l] = 0;
@@ -2980,6 +2900,14 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     for (int k = 0; k < 3; k++)
         if (cfg.grid[k] != scene.grid_dim[k]) { last_error = "config grid dims differ from the scene build"; return -1; }
     if (cfg.accel != ACCEL_GRID && scene.bvh_nodes.empty()) { last_error = "scene built without BVH"; return -1; }
+    if (cfg.accel != ACCEL_GRID)     // every BLAS path walks the 4-wide BLAS: there is no binary fallback
+        for (const ModelRec& m : scene.model_recs)
+            if (m.bvh_root >= 0 && (m.bvh4_root < 0 || scene.bvh4_nodes.empty())) {
+                last_error = "a mesh has no 4-wide BLAS (a leaf of more than 31 triangles, 2^26 leaf records or more "
+                             "in one mesh, or 2^27 4-wide nodes in the scene: beyond the traversal stacks' "
+                             "encodings); use accel grid";
+                return -1;
+            }
     for (const Voxel& v : scene.voxels)
         if (v.entity_type != ENTITY_TRIANGLE) { last_error = "unsupported voxel entity type"; return -1; }
     freeBuffers();
@@ -2992,6 +2920,7 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         npipes = std::max(1, std::min(kMaxPipes, pe ? std::atoi(pe) : cfg.pipelines));
     }
     kp = KParams{};
+    kp.defer_launch = 1;
     kp.nmodels = (int)scene.model_recs.size();
     for (int k = 0; k < 3; k++) kp.gdim[k] = scene.grid_dim[k];
     PT_HIP(upload(allocs, &kp.models, scene.model_recs.data(), scene.model_recs.size() * sizeof(ModelRec), stream));
@@ -3003,11 +2932,27 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         vox[i] = make_int2(scene.voxels[i].entity_index_range.start_index, scene.voxels[i].entity_index_range.end_index);
     PT_HIP(upload(allocs, &kp.voxels, vox.data(), vox.size() * sizeof(int2), stream));
     PT_HIP(upload(allocs, &kp.per_voxel, scene.per_voxel_data_pool.data(), scene.per_voxel_data_pool.size() * sizeof(int), stream));
-    PT_HIP(upload(allocs, &kp.bvh, scene.bvh_nodes.data(), scene.bvh_nodes.size() * sizeof(BvhNode), stream));
+    // one BLAS on the device: the 4-wide nodes every BLAS path walks (the binary build stays on the
+    // host, where the collapse reads it); leaf triangles inline in leaf order
     kp.bvh4 = nullptr;
     if (!scene.bvh4_nodes.empty())
         PT_HIP(upload(allocs, &kp.bvh4, scene.bvh4_nodes.data(), scene.bvh4_nodes.size() * sizeof(Bvh4Node), stream));
-    PT_HIP(upload(allocs, &kp.bvh_tri, scene.bvh_tri_order.data(), scene.bvh_tri_order.size() * sizeof(int), stream));
+    {   // PT_LDS_TOP: the two meshes with the most 4-wide nodes (the one after a root's range bounds it)
+        std::vector<std::pair<int, int>> ms;   // (node count, root)
+        std::vector<int> roots;
+        for (int r : scene.mesh_bvh4_root) if (r >= 0) roots.push_back(r);
+        std::sort(roots.begin(), roots.end());
+        roots.erase(std::unique(roots.begin(), roots.end()), roots.end());
+        for (size_t i = 0; i < roots.size(); i++) {
+            const int end = i + 1 < roots.size() ? roots[i + 1] : (int)scene.bvh4_nodes.size();
+            ms.push_back({end - roots[i], roots[i]});
+        }
+        std::sort(ms.rbegin(), ms.rend());
+        for (int m = 0; m < 2; m++) {
+            kp.top_root[m] = m < (int)ms.size() ? ms[m].second : 0;
+            kp.top_n[m] = m < (int)ms.size() ? std::min(ms[m].first, kLdsTop) : 0;
+        }
+    }
     PT_HIP(upload(allocs, &kp.bvh_tri_geom, scene.bvh_tri_geom.data(), scene.bvh_tri_geom.size() * sizeof(float), stream));
 
     kp.width = cfg.width;
@@ -3054,13 +2999,6 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         // value does not fail a render whose trace never reads it
         const bool gf_split = split_trace && cfg.accel == ACCEL_GRID_FAST;
         const bool bvh_split = split_trace && cfg.accel == ACCEL_BVH;
-        if ((gf_split && kGfBvh4) || (bvh_split && PT_BVH_BVH4)) {   // this build's traces walk the 4-wide BLAS only
-            for (const ModelRec& m : scene.model_recs)
-                if (m.bvh_root >= 0 && (m.bvh4_root < 0 || scene.bvh4_nodes.empty())) {
-                    last_error = "4-wide build: a mesh has no 4-wide BLAS (a leaf too large for the stack encoding)";
-                    return -1;
-                }
-        }
         gf_flags = gff && gf_split ? std::atoi(gff) : 9;
         if (gf_flags != 8 && gf_flags != 9) { last_error = "PT_GF_FLAGS must be 8 or 9"; return -1; }
         // 9..12 instances: the default variants with room for 12 LDS model records (F | 32)
@@ -3096,10 +3034,18 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* mb = std::getenv("PT_TRACE_MIN_WAVES_PER_CU");
         kp.trace_min_blocks = std::max(1, cus) * (mb ? std::max(1, std::atoi(mb)) : 2);
         // k_trace_gf's 12-entry LDS stack; k_trace_bvh's 4-wide traversal (up to three pushes per node)
-        const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || (cfg.accel == ACCEL_BVH && PT_BVH_BVH4));
+        const bool spills = split_trace && (cfg.accel == ACCEL_GRID_FAST || cfg.accel == ACCEL_BVH);
         // drain continuations
         const char* dd = std::getenv("PT_DRAIN_DUMP");
         kp.drain_dump = split_trace ? std::max(0, std::min(64, dd ? std::atoi(dd) : 16)) : 0;
+        const char* ddt = std::getenv("PT_DRAIN_DUMP_TAIL");  // a tail that hands on again (PT_DRAIN_LEVELS > 1)
+        kp.drain_dump_tail = ddt ? std::max(0, std::min(64, std::atoi(ddt))) : kp.drain_dump;
+        const char* trp = std::getenv("PT_TAIL_RPL");
+        kp.tail_rpl = trp ? std::max(1, std::atoi(trp)) : 1;
+        const char* dfl = std::getenv("PT_DEFER_LAUNCH");
+        kp.defer_launch = dfl ? std::atoi(dfl) != 0 : 1;
+        const char* trf = std::getenv("PT_TAIL_REFILL");
+        kp.tail_refill = trf ? std::max(1, std::min(64, std::atoi(trf))) : kp.trace_refill;
         kp.cont_cap = kp.drain_dump > 0 ? trace_blocks * 64 : 1;
         // walk hand-ons (k_trace_gf main launch -> its level-1 tail): room for one per lane
         // (PT_WALK_WCAP overrides; beyond it a ray goes whole to k_trace_deferred).  With one
@@ -3259,7 +3205,8 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b, l);
         }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
-        hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, PT_DEFER_WGS)), t, 0, st, k, b);
+        if (k.defer_launch)
+            hipLaunchKernelGGL(k_trace_deferred<64>, dim3((unsigned)std::min(trace_blocks, PT_DEFER_WGS)), t, 0, st, k, b);
         return;
     }
     // k_trace_bvh: 11 (LDS records), 43 (11 with room for 12), 10 (records in global memory)

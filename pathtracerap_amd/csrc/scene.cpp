@@ -598,7 +598,7 @@ void Scene::buildDeviceTables() {
         // computeRayGridIntersection uses models[grid.entity_index]'s mesh bbox == this mesh's.
         for (int k = 0; k < 3; k++) r.vw[k] = g.voxel_width[k];
         r.vox_start = g.voxelIndices.start_index;
-        r.mesh = m.mesh_index;
+        r.leaf_base = mesh_leaf_base.empty() ? 0 : mesh_leaf_base[m.mesh_index];
         r.tri_start = mesh.triangle_indices.start_index;
         r.tri_end = mesh.triangle_indices.end_index;
         r.bvh_root = mesh_bvh_root.empty() ? -1 : mesh_bvh_root[m.mesh_index];

@@ -97,6 +97,7 @@ public:
     std::vector<int> mesh_bvh_root;
     std::vector<Bvh4Node> bvh4_nodes; // the same BLAS collapsed 4-wide (k_trace_gf), all meshes
     std::vector<int> mesh_bvh4_root;  // -1: no 4-wide BLAS (empty mesh, or a leaf the encoding cannot hold)
+    std::vector<int> mesh_leaf_base;  // the mesh's first bvh_tri_order entry (4-wide leaf entries are relative)
 
     RenderSettings settings;          // optional RENDER block of the config
     std::string last_error;

@@ -42,16 +42,18 @@ def main():
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)          # read by allocateOnGPU
         acc = {"bvh": P.ACCEL_BVH, "grid": P.ACCEL_GRID, "grid_fast": P.ACCEL_GRID_FAST}[accel]
-        if acc not in scenes:
+        # build-time variables (PT_BVH*: read by Scene::build) get a scene of their own
+        skey = (acc, tuple(sorted((k, v) for k, v in env.items() if k.startswith("PT_BVH"))))
+        if skey not in scenes:
             if a.inmem and not a.scene:
                 s = synthetic.build_scene(P, ntri=a.ntri)
             else:
                 s = P.Scene(path)
                 s.build(bvh=acc != P.ACCEL_GRID)
-            scenes[acc] = s
+            scenes[skey] = s
         cfg = P.RenderConfig(width=a.width, height=a.height, max_bounces=a.bounces, accel=acc, block=int(block))
         r = P.Renderer(cfg)
-        r.allocateOnGPU(scenes[acc])
+        r.allocateOnGPU(scenes[skey])
         for k, old in saved.items():
             if old is None:
                 os.environ.pop(k, None)

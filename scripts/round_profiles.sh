@@ -7,11 +7,14 @@
 #   part 2 -- the north_star target (1M triangles) and configs[4] (10M triangles, 16
 #     bounces, scene built in memory), grid_fast: the same stats / FETCH / WRITE / SQ /
 #     wave-cycle passes, so bench.py's targets.*.roofline has its own traffic and issue
+#   part 3 -- configs[2] (the README scene, scenes/reference_scene.txt, at 2800x2240 and
+#     its RENDER block's 5 bounces; metal / coat / diffuse / emissive models): the same
+#     passes under bench.py's target key grid_fast_configs2_2800x2240_b5
 # Every pass runs --no-full-runs: the counters are per launch, and the SQ per-iteration
 # totals divide by the first-bounce dispatches the pass counted (scripts/pmc_summary.py).
 # scripts/pmc_summary.py folds the counters into gpurun_out/pmc_round.json (copy to
 # profiles/pmc_latest.json, which bench.py reads) and the stats CSVs go to gpurun_out/round/.
-#   usage: bash scripts/round_profiles.sh 1|2
+#   usage: bash scripts/round_profiles.sh 1|2|3
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 part=${1:-1}
@@ -46,6 +49,21 @@ if [ "$part" = 1 ]; then
   python3 scripts/pmc_table.py gpurun_out/s11_counters > gpurun_out/round/sq_cycles_p1.txt &&
   python3 scripts/pmc_table.py gpurun_out/s12_counters > gpurun_out/round/sq_cycles_16p.txt || exit 1
   echo "part 1: gpurun_out/round/, $O"
+elif [ "$part" = 3 ]; then
+  C="$B --scene scenes/reference_scene.txt --width 2800 --height 2240"
+  KC=grid_fast_configs2_2800x2240_b5
+  bash scripts/gpu_run.sh \
+    "prof=$C --steps 16" "prof=$C --steps 16 --pipelines 1" "pmc=$C $S --pipelines 1" \
+    "counters=$INS@$C $S --pipelines 1" "counters=$CYC@$C $S --pipelines 1" "counters=$CYC@$C $S" || exit $?
+  [ -f $O ] || cp profiles/pmc_latest.json $O
+  python3 scripts/pmc_summary.py $KC gpurun_out/s3_pmc_fetch gpurun_out/s3_pmc_write $O > /dev/null &&
+  python3 scripts/pmc_summary.py sq $KC gpurun_out/s4_counters _sq_p1 $O > /dev/null &&
+  python3 scripts/pmc_summary.py cycles $KC gpurun_out/s5_counters _cycles_p1 $O > /dev/null &&
+  python3 scripts/pmc_summary.py cycles $KC gpurun_out/s6_counters _cycles $O > /dev/null || exit 1
+  stats 1 grid_fast_configs2_16p && stats 2 grid_fast_configs2_1p || exit 1
+  python3 scripts/pmc_table.py gpurun_out/s5_counters > gpurun_out/round/sq_cycles_configs2_p1.txt &&
+  python3 scripts/pmc_table.py gpurun_out/s6_counters > gpurun_out/round/sq_cycles_configs2_16p.txt || exit 1
+  echo "part 3: gpurun_out/round/, $O"
 else
   M="$B --ntri 1000000"; T="$B --ntri 10000000 --bounces 16 --inmem"
   K1=grid_fast_1000000_1280x1024_b8; KT=grid_fast_10000000_1280x1024_b16

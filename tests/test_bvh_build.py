@@ -85,8 +85,9 @@ def test_depth_cap_on_degenerate_distribution(pt_mod):
 
 
 
-def _walk4(nodes, root):
-    """Leaves (first, count, box) and depth of a 4-wide BLAS (Bvh4Node rows)."""
+def _walk4(nodes, root, base=0):
+    """Leaves (first, count, box) and depth of a 4-wide BLAS (Bvh4Node rows);
+    `base` = the mesh's leaf_base, which the mesh-relative leaf links add back."""
     ints = nodes.view(np.int32)
     leaves, depth_max, seen = [], 0, set()
     stack = [(root, 1)]
@@ -105,15 +106,18 @@ def _walk4(nodes, root):
             else:                          # a leaf's link is its stack entry: 1 << 31 | count << 26 | first
                 e = int(ints[n, 24 + c]) & 0xFFFFFFFF
                 assert e >> 31 == 1 and (e >> 26) & 31 == count
-                leaves.append((e & ((1 << 26) - 1), count, box))
+                leaves.append((base + (e & ((1 << 26) - 1)), count, box))
     return leaves, depth_max, seen
 
 
+@pytest.mark.parametrize("order", ["0", "1"])
 @pytest.mark.parametrize("ntri", [10, 5000, 60000])
-def test_bvh4_collapse_keeps_every_leaf_box_bit_for_bit(pt_mod, ntri):
+def test_bvh4_collapse_keeps_every_leaf_box_bit_for_bit(pt_mod, monkeypatch, ntri, order):
     """The 4-wide BLAS (k_trace_gf's node steps) holds exactly the binary
     BLAS's leaves, with the same boxes bit for bit, in fewer nodes; every
-    leaf fits the traversal stack's leaf encoding."""
+    leaf fits the traversal stack's leaf encoding.  Breadth-first (default)
+    and depth-first (PT_BVH4_ORDER=1) node numbering alike."""
+    monkeypatch.setenv("PT_BVH4_ORDER", order)
     from pathtracerap_amd.synthetic import torus_mesh
     pos, nrm, tris = torus_mesh(ntri, seed=1)
     s = pt_mod.Scene()
@@ -123,7 +127,7 @@ def test_bvh4_collapse_keeps_every_leaf_box_bit_for_bit(pt_mod, ntri):
     b, b4 = s.export_bvh(), s.export_bvh4()
     leaves2, depth2 = _walk(b["nodes"], b["roots"][0])
     assert b4["roots"][0] >= 0
-    leaves4, depth4, seen = _walk4(b4["nodes"], b4["roots"][0])
+    leaves4, depth4, seen = _walk4(b4["nodes"], b4["roots"][0], b4["leaf_base"][0])
     assert len(seen) == len(b4["nodes"])          # no orphan nodes
     key = lambda lv: (lv[0], lv[1], lv[2][0].tobytes(), lv[2][1].tobytes())
     assert sorted(map(key, leaves4)) == sorted(map(key, leaves2))
@@ -138,25 +142,69 @@ def test_bvh4_roots_for_every_mesh_of_the_reference_scene(pt_mod):
     assert (b4["roots"] >= 0).all() and len(b4["nodes"]) > 0
 
 
-@pytest.mark.parametrize("ntri", [10, 5000])
+def _tiny_mesh(n):
+    """n disjoint triangles (n = 0: a mesh with no triangles)."""
+    pos = np.zeros((3 * n, 3), np.float32)
+    for i in range(n):
+        pos[3 * i:3 * i + 3] = np.float32([[i, 0, 0], [i + 0.5, 0, 0], [i, 0.5, 0.2]])
+    nrm = np.tile(np.float32([0, 0, 1]), (3 * n, 1))
+    return pos, nrm, np.arange(3 * n, dtype=np.int32).reshape(-1, 3)
+
+
+@pytest.mark.parametrize("ntri", [1, 2, 3, 10, 5000])
 def test_bvh4_empty_slots_are_inverted_infinite_boxes(pt_mod, ntri):
     """The node steps never read Bvh4Node.count: an empty slot must miss the
     near / far slab test by itself, which the inverted infinite box
-    (lo = +inf, hi = -inf) guarantees for every ray (entry +inf, exit -inf).
+    (lo = +inf, hi = -inf) guarantees for every ray (entry +inf, exit -inf),
+    with link -1.  That holds for slots past the children and for an empty
+    binary child (a 1- or 2-triangle mesh: a root leaf beside an empty child).
     Every other slot's box is finite and ordered."""
     from pathtracerap_amd.synthetic import torus_mesh
-    pos, nrm, tris = torus_mesh(ntri, seed=2)
+    pos, nrm, tris = torus_mesh(ntri, seed=2) if ntri >= 10 else _tiny_mesh(ntri)
     s = pt_mod.Scene()
     m = s.addMesh(pos, nrm, tris)
     s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
     s.build(bvh=True)
-    nodes = s.export_bvh4()["nodes"]
+    b4 = s.export_bvh4()
+    nodes = b4["nodes"]
+    assert b4["roots"][0] >= 0 and len(nodes) > 0
     ints = nodes.view(np.int32)
     empty = ints[:, 28:32] < 0
     lo = np.stack([nodes[:, 0:4], nodes[:, 4:8], nodes[:, 8:12]])
     hi = np.stack([nodes[:, 12:16], nodes[:, 16:20], nodes[:, 20:24]])
-    assert empty.any() or ntri > 10       # a 10-triangle mesh leaves slots empty
+    assert empty.any() or ntri > 10       # a small mesh leaves slots empty
     assert (lo[:, empty] == np.inf).all() and (hi[:, empty] == -np.inf).all()
+    assert (ints[:, 24:28][empty] == -1).all() and (ints[:, 28:32][empty] == -1).all()
     full = ~empty
     assert np.isfinite(lo[:, full]).all() and np.isfinite(hi[:, full]).all()
     assert (lo[:, full] <= hi[:, full]).all()
+    leaves, _, _ = _walk4(nodes, b4["roots"][0], b4["leaf_base"][0])
+    assert sum(c for _, c, _ in leaves) == len(tris)
+
+
+def test_bvh4_leaf_links_are_relative_to_their_mesh(pt_mod):
+    """A 4-wide leaf link holds its first record relative to the mesh's
+    leaf_base (ModelRec::leaf_base, added back by the traces), so the 2^26
+    limit of the stack's leaf encoding applies per mesh: every mesh's
+    smallest relative first is 0, and leaf_base + first gives exactly the
+    binary BLAS's leaves of that mesh, whatever precedes it in bvh_tri_order."""
+    from pathtracerap_amd.synthetic import torus_mesh
+    s = pt_mod.Scene()
+    sizes = [5000, 1, 300, 2, 12000]
+    for i, n in enumerate(sizes):
+        pos, nrm, tris = torus_mesh(n, seed=5 + i) if n >= 10 else _tiny_mesh(n)
+        m = s.addMesh(pos + np.float32(3 * i), nrm, tris)
+        s.addModel(m, (1, 1, 1), (0, 0, 0), (0, 0, 0), "DIFFUSE", (1, 1, 1))
+        sizes[i] = len(tris)
+    s.build(bvh=True)
+    b, b4 = s.export_bvh(), s.export_bvh4()
+    assert (b4["roots"] >= 0).all()
+    assert b4["leaf_base"][0] == 0 and (np.diff(b4["leaf_base"]) > 0).all()
+    key = lambda lv: (lv[0], lv[1], lv[2][0].tobytes(), lv[2][1].tobytes())
+    for mi, n in enumerate(sizes):
+        rel, _, _ = _walk4(b4["nodes"], b4["roots"][mi])
+        assert min(f for f, _, _ in rel) == 0
+        abs4, _, _ = _walk4(b4["nodes"], b4["roots"][mi], b4["leaf_base"][mi])
+        leaves2, _ = _walk(b["nodes"], b["roots"][mi])
+        assert sorted(map(key, abs4)) == sorted(map(key, leaves2))
+        assert sum(c for _, c, _ in abs4) == n

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(pt_mod):
 
 def test_abi_version_and_defaults(pt_mod):
     L = pt_mod.lib()
-    assert L.pt_abi_version() == 7
+    assert L.pt_abi_version() == 8
     c = pt_mod._Cfg()
     L.pt_default_config(ctypes.byref(c))
     # Config.h / generateRaysKernel defaults

@@ -227,3 +227,20 @@ def test_cli_defaults_equal_oracle(gpu, pt_mod, tmp_path):
     assert p.returncode == 0, p.stderr
     assert "Mrays/s" in p.stdout
     assert np.array_equal(_bmp_payload(out), _oracle_bmp_payload())
+
+
+def test_configs4_10m_triangles_320x256_grid_fast_equals_grid(gpu, pt_mod, scene_10m):
+    """configs[4]'s view on a whole 320x256 frame, 16 bounces: the benched
+    grid_fast path (4-wide node steps, ray sort, sparse-bounce launch sizing,
+    drain and walk hand-ons) against the reference grid mode (the list-walking
+    DDA, the literal restatement of Renderer.cpp:238-360), image and every
+    bounce's live-ray count bit for bit -- whole-frame coverage beside the
+    five oracle windows."""
+    P = pt_mod
+    small = P.RenderConfig(width=320, height=256, iterations=1, max_bounces=16)
+    a = _gpu_render(P, scene_10m, small)
+    small.accel = P.ACCEL_GRID
+    b = _gpu_render(P, scene_10m, small)
+    assert a["faults"] == 0 and b["faults"] == 0
+    assert a["per_bounce"] == b["per_bounce"]
+    assert_bitexact(a["img"], b["img"], "grid_fast vs grid, 10M triangles, 320x256")

@@ -525,6 +525,32 @@ def test_drain_continuation_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, mo
 
 
 @pytest.mark.parametrize("accel", [1, 2])
+@pytest.mark.parametrize("rpl,refill,levels,dump_tail", [("2", "32", "1", "16"), ("4", "16", "1", "16"),
+                                                         ("1000000", "8", "1", "16"), ("3", "32", "2", "8"),
+                                                         ("1", "48", "3", "32")])
+def test_tail_sized_to_records_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, rpl, refill,
+                                             levels, dump_tail):
+    """PT_TAIL_RPL / PT_TAIL_REFILL / PT_DRAIN_DUMP_TAIL: a tail launch runs only
+    ceil(records / (64 * rpl)) waves, whose lanes claim further records once
+    `refill` of them are idle, and a tail that hands on again uses its own
+    drain threshold.  Only which lane resumes which record, and when, changes:
+    images and segment counts stay the oracle's, down to one tail wave."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_DRAIN_DUMP", "24")
+    monkeypatch.setenv("PT_DRAIN_LEVELS", levels)
+    monkeypatch.setenv("PT_TAIL_RPL", rpl)
+    monkeypatch.setenv("PT_TAIL_REFILL", refill)
+    monkeypatch.setenv("PT_DRAIN_DUMP_TAIL", dump_tail)
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=6000, seed=13, metallic=True))
+    s.build(bvh=True)
+    cfg = P.RenderConfig(width=211, height=97, iterations=3, max_bounces=7, accel=accel, pipelines=4)
+    img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+    assert seg == oseg
+    assert_bitexact(img, oimg, f"PT_TAIL_RPL={rpl} PT_TAIL_REFILL={refill} levels={levels}")
+
+
+@pytest.mark.parametrize("accel", [1, 2])
 @pytest.mark.parametrize("rpl,minw", [("0", "2"), ("4", "2"), ("64", "1"), ("1000000", "1")])
 def test_main_launch_sized_to_the_rays_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, rpl, minw):
     """PT_TRACE_RPL: a bounce whose rays come to fewer than rpl per lane runs only

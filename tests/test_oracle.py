@@ -71,6 +71,41 @@ def test_minstd_uniform_first_draw(oracle_mod):
         assert np.float32(L.ptor_u01_first(*args)) == first(*args)
 
 
+def test_seeding_at_the_iteration_ids_the_bench_publishes(oracle_mod):
+    """utility.h:58-62 at the ids of the full-spp runs: iterations up to 4095
+    (configs[4]: 4096 spp) at depth 16, 1023 (1M target, configs[2]) at depth 8
+    and 5, 255 (configs[1]), for the first, middle and last pixel slots.  The
+    seed word (1 << 31) | depth << 22 | iter keeps depth and iter apart up to
+    iter 2^22 - 1; past it they overlap by OR, as in the reference."""
+    m = 0xFFFFFFFF
+
+    def h(a):
+        a = ((a + 0x7ed55d16) + (a << 12)) & m
+        a = ((a ^ 0xc761c23c) ^ (a >> 19)) & m
+        a = ((a + 0x165667b1) + (a << 5)) & m
+        a = ((a + 0xd3a2646c) ^ (a << 9)) & m
+        a = ((a + 0xfd7046c5) + (a << 3)) & m
+        a = ((a ^ 0xb55a4f09) ^ (a >> 16)) & m
+        return a
+
+    def first(iter_, index, depth):
+        word = (0x80000000 | (depth << 22) | iter_) & m   # int arithmetic on 32 bits, as in the reference
+        x = (h(word) ^ h(index)) % 2147483647 or 1          # thrust minstd seed: s mod m, 0 -> 1
+        x = (x * 48271) % 2147483647
+        return np.float32(np.float32(x - 1) / np.float32(2147483648.0))
+
+    L = oracle_mod.lib()
+    npix = 1280 * 1024
+    cases = [(4095, i, d) for i in (0, npix // 2, npix - 1) for d in (16, 9, 1)]
+    cases += [(1023, i, d) for i in (0, 777_777, npix - 1) for d in (8, 5, 1)]
+    cases += [(1023, 2800 * 2240 - 1, 5), (255, 1_000_000, 8), (254, 3, 7), ((1 << 22) - 1, 42, 16),
+              (1 << 22, 42, 16), (4095, 0x7FFFFFFF, 16)]
+    for args in cases:
+        assert np.float32(L.ptor_u01_first(*args)) == first(*args), args
+    # depth 16 and iter 4095 occupy disjoint bits; the overlap only starts at iter 2^22
+    assert (16 << 22) & 4095 == 0 and (16 << 22) & (1 << 22) == 0
+
+
 def test_bmp_writer_matches_reference_layout(oracle_mod):
     img = np.zeros((2 * 3, 3), np.float32)
     img[0] = [1.0, 0.5, 0.0]      # (x=0,y=0) -> bytes 255,127,0 in x,y,z order
