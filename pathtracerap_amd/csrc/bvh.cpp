@@ -333,6 +333,9 @@ void Scene::buildBvh4() {
             }
         }
         if (base < 0) base = 0;
+#if defined(PT_LEAF_REL) && PT_LEAF_REL == 0
+        base = 0;                        // absolute leaf links (timing experiments)
+#endif
         // make(b): the 4-wide node for binary node b; returns its index
         std::vector<std::pair<int, int>> work;   // (binary node, 4-wide index) still to fill
         auto alloc = [&](int b) {

@@ -97,6 +97,8 @@ struct KParams {
                                         // once, so each lane resumes about tail_rpl records (PT_TAIL_RPL; 1 =
                                         // one wave per 64 records)
     int tail_refill;                    // a tail wave claims more records once this many lanes are idle
+    int allphase_lanes;                 // k_trace_gf: every step kind each iteration once the rays are claimed
+                                        // and at most this many lanes trace (PT_ALLPHASE_LANES; 0 = off)
     int defer_launch;                   // 0: k_trace_deferred is not launched (PT_DEFER_LAUNCH=0, timing
                                         // experiments); k_scan then counts a trace fault if any ray was deferred
     unsigned trace_iter_cap;            // persistent traces give up after this many loop iterations (a fault,

@@ -1286,6 +1286,12 @@ __device__ __forceinline__ int spop_if(bool take, const int* stack, const int* s
     return v;
 }
 
+#ifndef PT_LEAF_REL
+#define PT_LEAF_REL 1         // 4-wide leaf links relative to ModelRec::leaf_base (0: absolute; timing experiments)
+#endif
+#ifndef PT_EMPTY_SKIP
+#define PT_EMPTY_SKIP 1       // the traces' select steps skip models whose mesh has no triangles
+#endif
 #ifndef PT_LEAF_STEP
 #define PT_LEAF_STEP 2        // leaf triangles tested per leaf step of k_trace_bvh (1..4; k_trace_gf: 1 or 2)
 #endif
@@ -1570,7 +1576,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                     node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
                     if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;
                 } else if (model_culled<ACCEL_BVH>(M, ow, dw, winv, dlen, gdist)) continue;
-                if (M.bvh4_root < 0) continue;              // a mesh without triangles: no hit, no BLAS
+                if (PT_EMPTY_SKIP && M.bvh4_root < 0) continue;   // a mesh without triangles: no hit, no BLAS
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -1614,7 +1620,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
             const int top = spop_if<BS, kStack>(pop, stack, spill, p.spill_stride, sp - 1);
             sp -= pop ? 1 : 0;
             const bool tleaf = pop & (top < 0);
-            const int first = lbase + (top & ((1 << kLeafCountShift) - 1));   // mesh-relative entry
+            const int first = (PT_LEAF_REL ? lbase : 0) + (top & ((1 << kLeafCountShift) - 1));   // mesh-relative entry
             lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
             lf_i = tleaf ? first : lf_i;
             cur = (pop & !tleaf) ? top : cur;
@@ -1667,7 +1673,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 sp -= pop ? 1 : 0;
                 const int nx = nhit > 0 ? ent[0] : top;
                 const bool leaf = !model_done & (nx < 0);
-                const int first = lbase + (nx & ((1 << kLeafCountShift) - 1));
+                const int first = (PT_LEAF_REL ? lbase : 0) + (nx & ((1 << kLeafCountShift) - 1));
                 lf_i = leaf ? first : lf_i;
                 lf_e = leaf ? first + ((nx >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
                 cur = (!model_done & !leaf) ? nx : cur;
@@ -1900,7 +1906,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     if (kLdsTop > 0) {
         const float4* nodes4 = reinterpret_cast<const float4*>(p.bvh4);
         for (int i = threadIdx.x; i < kLdsTopMeshes * kLdsTop * 8; i += BS) {
-            const int m = i / (kLdsTop * 8), k = (i / 8) % kLdsTop;
+            constexpr int kT = kLdsTop > 0 ? kLdsTop : 1;
+            const int m = i / (kT * 8), k = (i / 8) % kT;
             s_top[i] = k < p.top_n[m] ? nodes4[8 * (size_t)(p.top_root[m] + k) + (i & 7)] : make_float4(0, 0, 0, 0);
         }
         __syncthreads();
@@ -2051,6 +2058,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (c5 * 4 > cm * PT_WALK_W) { phase = 8; cm = c5; }
             if (c1 * 4 > cm * PT_SEL_W) { phase = 1; cm = c1; }
         }
+        // once the rays are claimed and few lanes still trace (PT_ALLPHASE_LANES; experiment, 0 = off),
+        // every step kind runs every iteration: no lane waits for the other lanes' phases
+        if (exhausted && p.allphase_lanes > 0 && __popcll(__ballot(state != 3)) <= p.allphase_lanes) phase = 1 | 2 | 4 | 8;
         // drain: at most drain_dump lanes still trace once the pool is exhausted
         {
             const int dd = TAIL ? p.drain_dump_tail : p.drain_dump;
@@ -2109,7 +2119,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     node_slab(M.wbox, M.wbox + 3, ow, winv, wtn, wtf);
                     if (wtn * dlen > gdist * 1.0001f + 0.01f) continue;
                 } else if (model_culled<ACCEL_GRID_FAST>(M, ow, dw, winv, dlen, gdist)) continue;
-                if (M.bvh4_root < 0) continue;              // a mesh without triangles: no hit, no BLAS
+                if (PT_EMPTY_SKIP && M.bvh4_root < 0) continue;   // a mesh without triangles: no hit, no BLAS
                 o = xform12(M.w2m, ow, 1.0f);
                 d = normalize(xform12(M.w2m, dw, 0.0f));
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -2212,7 +2222,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 const int top = spop_if<BS, kGfStack>(pop, stack, spill, p.spill_stride, sp - 1);
                 sp -= pop ? 1 : 0;
                 const bool tleaf = pop & (top < 0);
-                const int first = lbase + (top & ((1 << kLeafCountShift) - 1));   // mesh-relative entry
+                const int first = (PT_LEAF_REL ? lbase : 0) + (top & ((1 << kLeafCountShift) - 1));   // mesh-relative entry
                 lf_e = tleaf ? first + ((top >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
                 lf_i = tleaf ? first : lf_i;
                 cur = (pop & !tleaf) ? top : cur;
@@ -2303,7 +2313,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 sp -= pop ? 1 : 0;
                 const int nx = nhit > 0 ? ent[0] : top;       // the entry to go on with (when not collected)
                 const bool leaf = !collected & (nx < 0);
-                const int first = lbase + (nx & ((1 << kLeafCountShift) - 1));
+                const int first = (PT_LEAF_REL ? lbase : 0) + (nx & ((1 << kLeafCountShift) - 1));
                 lf_i = leaf ? first : lf_i;
                 lf_e = leaf ? first + ((nx >> kLeafCountShift) & kMaxLeafCount4) : lf_e;
                 cur = (!collected & !leaf) ? nx : cur;
@@ -2441,6 +2451,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     if (stamps && lane == 0) {
         for (int q = 0; q < 6; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
         for (int q = 0; q < 4; q++) atomicAdd(p.segments + 55 + q + kMaxBounceCounters, cyr[q]);
+        if (TAIL)                                   // the tail launches' own cycle split (slots 70..75)
+            for (int q = 0; q < 6; q++) atomicAdd(p.segments + 70 + q + kMaxBounceCounters, cy[q]);
     }
     if ((PT_TRACE_STATS && (p.debug & 16)) && lane == 0) {
         atomicAdd(p.segments + 8 + kMaxBounceCounters, st_iter);
@@ -3042,6 +3054,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.drain_dump_tail = ddt ? std::max(0, std::min(64, std::atoi(ddt))) : kp.drain_dump;
         const char* trp = std::getenv("PT_TAIL_RPL");
         kp.tail_rpl = trp ? std::max(1, std::atoi(trp)) : 1;
+        const char* apl = std::getenv("PT_ALLPHASE_LANES");
+        kp.allphase_lanes = apl ? std::max(0, std::min(64, std::atoi(apl))) : 0;
         const char* dfl = std::getenv("PT_DEFER_LAUNCH");
         kp.defer_launch = dfl ? std::atoi(dfl) != 0 : 1;
         const char* trf = std::getenv("PT_TAIL_REFILL");

@@ -111,6 +111,11 @@ def main():
             tot = max(sum(cyc), 1)
             out[v]["cycle_share"] = dict(zip(["refill", "select", "leaf", "node", "walk", "handon_drain"],
                                              [round(c / tot, 3) for c in cyc]))
+            tc = allc[133:139]                       # slots 70..75: the tail launches' cycles by phase
+            if any(tc):
+                out[v]["tail_cycle_share_of_all"] = round(sum(tc) / tot, 3)
+                out[v]["tail_cycle_share"] = dict(zip(["resume", "select", "leaf", "node", "walk", "handon_drain"],
+                                                      [round(c / sum(tc), 3) for c in tc]))
             rr = allc[118:122]                       # slots 55..58: refill claim / order+gather / -, pre-refill
             out[v]["refill_split_share"] = dict(zip(["claim", "-", "order_and_gather", "stores_before"],
                                                     [round(c / tot, 3) for c in rr]))

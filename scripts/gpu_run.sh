@@ -82,7 +82,7 @@ for step in "$@"; do
           if [ "$lib" = default ]; then L=$PWD/pathtracerap_amd/libpathtracer_amd.so; else L=$PWD/build_variants/lib_$lib.so; fi
           PT_LIB_PATH=$L timeout -k 10 300 python scripts/ab.py --variants $spec --rounds 2 --steps 16 > gpurun_out/${tag}_$lib.json 2> gpurun_out/${tag}_$lib.err
           rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/${tag}_$lib.err; break 2; }
-          python3 -c "import json; d=json.load(open('gpurun_out/${tag}_$lib.json')); print('round $r $lib', {k: v['Mrays_s'] for k, v in d.items()})"
+          python3 -c "import json; d=json.load(open('gpurun_out/${tag}_$lib.json')); print('round $r $lib', {k: v['Mrays_s'] for k, v in d.items()})" | tee -a gpurun_out/${tag}_rounds.txt
         done
       done ;;
     abbench)
@@ -93,7 +93,7 @@ for step in "$@"; do
           if [ "$lib" = default ]; then L=$PWD/pathtracerap_amd/libpathtracer_amd.so; else L=$PWD/build_variants/lib_$lib.so; fi
           PT_LIB_PATH=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile --alt-accel= --targets= $bargs > gpurun_out/${tag}_$lib.json 2> gpurun_out/${tag}_$lib.err
           rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/${tag}_$lib.err; break 2; }
-          python3 -c "import json; d=json.load(open('gpurun_out/${tag}_$lib.json')); print('round $r $lib', d['value'], d['ms_per_step'])"
+          python3 -c "import json; d=json.load(open('gpurun_out/${tag}_$lib.json')); print('round $r $lib', d['value'], d['ms_per_step'])" | tee -a gpurun_out/${tag}_rounds.txt
         done
       done ;;
     py)

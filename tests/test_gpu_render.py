@@ -550,6 +550,26 @@ def test_tail_sized_to_records_bit_identical(gpu, pt_mod, oracle_mod, synth_dir,
     assert_bitexact(img, oimg, f"PT_TAIL_RPL={rpl} PT_TAIL_REFILL={refill} levels={levels}")
 
 
+@pytest.mark.parametrize("lanes,pipes", [("16", 4), ("64", 4), ("64", 1)])
+@pytest.mark.parametrize("scene", ["synthetic", "reference"])
+def test_allphase_iterations_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, lanes, pipes, scene):
+    """PT_ALLPHASE_LANES: once a k_trace_gf wave's rays are claimed and at most
+    `lanes` lanes still trace (the tail launches, a main launch's last rays),
+    every step kind runs in every iteration instead of the one most lanes wait
+    in.  Only which iteration a lane's step runs in changes: images and segment
+    counts stay the oracle's."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    monkeypatch.setenv("PT_ALLPHASE_LANES", lanes)
+    path = synthetic.diffuse_scene(synth_dir, ntri=6000, seed=13, metallic=True) if scene == "synthetic" else REF_SCENE
+    s = P.Scene(path)
+    s.build(bvh=True)
+    cfg = P.RenderConfig(width=211, height=97, iterations=3, max_bounces=7, accel=2, pipelines=pipes)
+    img, seg, oimg, oseg = _render_both(P, O, s, cfg)
+    assert seg == oseg
+    assert_bitexact(img, oimg, f"PT_ALLPHASE_LANES={lanes} pipelines={pipes} {scene}")
+
+
 @pytest.mark.parametrize("accel", [1, 2])
 @pytest.mark.parametrize("rpl,minw", [("0", "2"), ("4", "2"), ("64", "1"), ("1000000", "1")])
 def test_main_launch_sized_to_the_rays_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, rpl, minw):
