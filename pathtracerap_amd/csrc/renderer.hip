@@ -894,8 +894,8 @@ __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelR
 
 template <int CAP, class GetM, bool CERT = true, bool STRICT = false>
 __device__ __forceinline__ WalkResult hitset_walk_g(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
-                                                    GetM get, int nh, float tmin, float win) {
-    if (CERT) {
+                                                    GetM get, int nh, float tmin, float win, bool try_cert = true) {
+    if (CERT && try_cert) {
         int tri;
         if (walk_certify<CAP>(p, M, d, inv, pt, t_box, get, nh, tmin, win, tri)) {
             if (PT_TRACE_STATS && (p.debug & 4)) atomicAdd(p.segments + 13 + kMaxBounceCounters, 1ull);
@@ -955,12 +955,12 @@ __device__ WalkResult hitset_walk(const KParams& p, const ModelRec& M, f3 d, f3 
 template <int CAP, int HSTRIDE, bool CERT = true, bool STRICT = false>
 __device__ __forceinline__ WalkResult hitset_walk_regs(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt,
                                                        float t_box, const int4* __restrict__ hs, int nh, float tmin,
-                                                       float win) {
+                                                       float win, bool try_cert = true) {
     int4 mem[CAP];
 #pragma unroll
     for (int h = 0; h < CAP; h++) mem[h] = h < nh ? hs[h * HSTRIDE] : make_int4(0, 0, 0, 0);
     auto get = [&](int h) { return mem[h]; };
-    return hitset_walk_g<CAP, decltype(get), CERT, STRICT>(p, M, d, inv, pt, t_box, get, nh, tmin, win);
+    return hitset_walk_g<CAP, decltype(get), CERT, STRICT>(p, M, d, inv, pt, t_box, get, nh, tmin, win, try_cert);
 }
 
 // Overflow tiers of grid_hitset: bounded, then unbounded collection into a
@@ -1444,8 +1444,15 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                         lf_next = C[kCLfNext * cs];
                         sbase = C[kCSpill * cs]; spill = p.spill + sbase;
                         best = __int_as_float(C[kCX * cs]); best_tri = C[(kCX + 1) * cs]; any = C[(kCX + 2) * cs] != 0;
+                        // the live stack entries only, four loads in flight at a time (one wait per four)
 #pragma unroll 1
-                        for (int q = 0; q < kStack; q++) stack[q * BS] = C[(kCX + 3 + q) * cs];
+                        for (int q0 = 0; q0 < min(sp, kStack); q0 += 4) {
+                            int v[4];
+#pragma unroll
+                            for (int k = 0; k < 4; k++) v[k] = C[(kCX + 3 + min(q0 + k, kStack - 1)) * cs];
+#pragma unroll
+                            for (int k = 0; k < 4; k++) if (q0 + k < kStack) stack[(q0 + k) * BS] = v[k];
+                        }
                         winv = node_inv(cull_inv(dw));
                         dlen = sqrtf(dot(dw, dw));
                         if (state != 1) {                   // inside model im: its model-space ray, as selected
@@ -1545,7 +1552,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
                 C[kCLfNext * cs] = lf_next; C[kCSpill * cs] = sbase;
                 C[kCX * cs] = __float_as_int(best); C[(kCX + 1) * cs] = best_tri; C[(kCX + 2) * cs] = any ? 1 : 0;
 #pragma unroll 1
-                for (int q = 0; q < kStack; q++) C[(kCX + 3 + q) * cs] = stack[q * BS];
+                for (int q = 0; q < min(sp, kStack); q++) C[(kCX + 3 + q) * cs] = stack[q * BS];
             }
             state = 3;
         }
@@ -1916,7 +1923,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     const int n = p.n_live[bounce];
     const int in_buf = (bounce + 1) & 1;
     const int lane = threadIdx.x & 63;
-    // lane state: 0 needs a ray, 1 select model, 2 node visit, 4 leaf triangle, 5 walk, 3 no more rays
+    // lane state: 0 needs a ray, 1 select model, 2 node visit, 4 leaf triangle, 5 walk, 3 no more rays,
+    // 6 walk handed on (main launch), 7 walk of a resumed hand-on (certificates already declined)
     int state = 0;
     int j = -1;
     f3 ow = mk3(0, 0, 0), dw = mk3(0, 0, 0);
@@ -1972,10 +1980,18 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     t_box = __int_as_float(C[(kCX + 5) * cs]);
                     G = mk3(__int_as_float(C[(kCX + 6) * cs]), __int_as_float(C[(kCX + 7) * cs]),
                             __int_as_float(C[(kCX + 8) * cs]));
+                    // the live stack entries and hit-set members only (a walk hand-on has no stack; a
+                    // pool-held hit set lives in its pool block), four loads in flight at a time
 #pragma unroll 1
-                    for (int q = 0; q < kGfStack; q++) stack[q * BS] = C[(kCX + 9 + q) * cs];
+                    for (int q0 = 0; q0 < min(sp, kGfStack); q0 += 4) {
+                        int v[4];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) v[k] = C[(kCX + 9 + min(q0 + k, kGfStack - 1)) * cs];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) if (q0 + k < kGfStack) stack[(q0 + k) * BS] = v[k];
+                    }
 #pragma unroll 1
-                    for (int q = 0; q < kGfHitCap; q++)
+                    for (int q = 0; q < (pblk < 0 ? nh : 0); q++)
                         hs[q * BS] = make_int4(C[(kCX + 9 + kGfStack + 4 * q) * cs], C[(kCX + 10 + kGfStack + 4 * q) * cs],
                                                C[(kCX + 11 + kGfStack + 4 * q) * cs], C[(kCX + 12 + kGfStack + 4 * q) * cs]);
                     if (state > 1) {                        // inside model im: its model-space ray, as selected
@@ -2052,7 +2068,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
         int phase = 2;
         {
             const int c1 = __popcll(__ballot(state == 1)), c2 = __popcll(__ballot(state == 2)),
-                      c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5));
+                      c4 = __popcll(__ballot(state == 4)), c5 = __popcll(__ballot(state == 5 || state == 7));
             int cm = c2;
             if (c4 * 4 > cm * PT_LEAF_W) { phase = 4; cm = c4; }
             if (c5 * 4 > cm * PT_WALK_W) { phase = 8; cm = c5; }
@@ -2076,7 +2092,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             }
             if (phase & 2) { st_node += __popcll(__ballot(state == 2)); it_node++; }
             if (phase & 4) { st_leaf += __popcll(__ballot(state == 4)); it_leaf++; }
-            if (phase & 8) { st_walk += __popcll(__ballot(state == 5)); it_walk++; }
+            if (phase & 8) { st_walk += __popcll(__ballot(state == 5 || state == 7)); it_walk++; }
             if (phase & 1) { st_sel += __popcll(__ballot(state == 1)); it_sel++; }
         }
         if (stamps) { const unsigned long long t = clock64(); cy[0] += t - ts; ts = t; }
@@ -2338,7 +2354,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 sp = 0; nh = 0; tmin = kFMax;
                 state = 2;
             }
-        } else if ((phase & 8) && state == 5) {          // the walk: certificate, else the exact walk
+        } else if ((phase & 8) && (state == 5 || state == 7)) {   // the walk: certificate, else the exact walk
             if (PT_TRACE_STATS && (p.debug & 2048))       // walks by hit-set size: 1, 2, 3, >= 4 (pool: >= 4)
                 atomicAdd(p.segments + 51 + (pblk >= 0 ? 3 : min(nh, 4) - 1) + kMaxBounceCounters, 1ull);
             const ModelRec& M = models[im];
@@ -2378,7 +2394,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 if (!ok) state = 6;
             } else {
                 const f3 inv = mk3(1 / d.x, 1 / d.y, 1 / d.z);
-                w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win)
+                // state 7: a walk hand-on whose LDS hit set both certificates already declined in
+                // the main launch (deterministically: they would decline again): the exact walk only
+                w = pblk < 0 ? hitset_walk_regs<kGfHitCap, BS, true, true>(p, M, d, inv, pt, t_box, hs, nh, tmin, win,
+                                                                            state != 7)
                              : hitset_walk<1, true>(p, M, d, inv, pt, t_box, p.hs_pool + (size_t)pblk * kHitCapPool, nh,
                                                     tmin, win);
             }
@@ -2421,7 +2440,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             if (mine) {
                 int* C = cout + (drain ? r : p.cont_cap - 1 - r);
                 const size_t cs = (size_t)p.cont_cap;
-                C[kCJ * cs] = j; C[kCState * cs] = drain ? state : 5; C[kCIm * cs] = im;
+                // a walk hand-on resumes in state 7 (walk, certificates already declined) unless its hit
+                // set is in a pool block, where the main launch tries no certificate
+                C[kCJ * cs] = j; C[kCState * cs] = drain ? state : (pblk < 0 ? 7 : 5); C[kCIm * cs] = im;
                 C[kCGdist * cs] = __float_as_int(gdist); C[kCGmodel * cs] = gmodel; C[kCGtri * cs] = gtri;
                 C[kCOw * cs] = __float_as_int(ow.x); C[(kCOw + 1) * cs] = __float_as_int(ow.y);
                 C[(kCOw + 2) * cs] = __float_as_int(ow.z);
@@ -2436,9 +2457,9 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                 C[(kCX + 6) * cs] = __float_as_int(G.x); C[(kCX + 7) * cs] = __float_as_int(G.y);
                 C[(kCX + 8) * cs] = __float_as_int(G.z);
 #pragma unroll 1
-                for (int q = 0; q < (drain ? kGfStack : 0); q++) C[(kCX + 9 + q) * cs] = stack[q * BS];
+                for (int q = 0; q < (drain ? min(sp, kGfStack) : 0); q++) C[(kCX + 9 + q) * cs] = stack[q * BS];
 #pragma unroll 1
-                for (int q = 0; q < kGfHitCap; q++) {
+                for (int q = 0; q < (pblk < 0 ? nh : 0); q++) {
                     const int4 e = hs[q * BS];
                     C[(kCX + 9 + kGfStack + 4 * q) * cs] = e.x; C[(kCX + 10 + kGfStack + 4 * q) * cs] = e.y;
                     C[(kCX + 11 + kGfStack + 4 * q) * cs] = e.z; C[(kCX + 12 + kGfStack + 4 * q) * cs] = e.w;
