@@ -1749,6 +1749,9 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
+#ifndef PT_HIT_LATE
+#define PT_HIT_LATE 0         // k_trace_gf: a finished ray's hit record stored behind the next claim (experiment)
+#endif
 #ifndef PT_LDS_TOP
 #define PT_LDS_TOP 0          // k_trace_gf: top 4-wide nodes per mesh staged in LDS (experiment; 0 = off)
 #endif
@@ -1935,6 +1938,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
+    constexpr bool kHitLate = PT_HIT_LATE != 0;
+    bool pend = false;                              // PT_HIT_LATE: this lane's finished ray's hit record not yet written
     int lbase = 0;                                  // ModelRec::leaf_base of the model being traced
     bool exhausted = false;
     unsigned cmask = 0;                            // PT_SEL_MASK: candidate models of the lane's ray
@@ -1955,6 +1960,11 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.cont_next + level - 1, cnt);
+            if (kHitLate && pend) {                                   // behind the claim
+                const int4 e = hs[0];
+                put_hit(p, e.w, __int_as_float(e.x), e.z, e.y);
+                pend = false;
+            }
             base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             if (base + cnt >= ncont) exhausted = true;
             if (state == 0) {
@@ -2023,6 +2033,11 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.trace_next, cnt);
+            if (kHitLate && pend) {                                   // behind the claim
+                const int4 e = hs[0];
+                put_hit(p, e.w, __int_as_float(e.x), e.z, e.y);
+                pend = false;
+            }
             base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             rstamp(0);
             if (base + cnt >= n) exhausted = true;
@@ -2125,7 +2140,11 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     im++;
                 }
                 if (im >= p.nmodels) {
-                    put_hit(p, j, gdist, gmodel, gtri);
+                    // PT_HIT_LATE: the hit record waits in the lane's (now unused) first hit-set slot
+                    // and is stored behind the next refill's claim, so that claim does not wait on
+                    // the record's store (vmcnt counts stores on gfx950)
+                    if (kHitLate) { hs[0] = make_int4(__float_as_int(gdist), gtri, gmodel, j); pend = true; }
+                    else put_hit(p, j, gdist, gmodel, gtri);
                     state = 0;
                     break;
                 }
@@ -2468,6 +2487,10 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             state = drain ? 3 : (state == 6 ? 0 : state);
         }
         if (stamps) { const unsigned long long t = clock64(); cy[5] += t - ts; ts = t; }
+    }
+    if (kHitLate && pend) {                         // lanes that finished after their wave's last claim
+        const int4 e = hs[0];
+        put_hit(p, e.w, __int_as_float(e.x), e.z, e.y);
     }
     if (stamps && lane == 0) {
         for (int q = 0; q < 6; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
