@@ -3042,7 +3042,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     PT_HIP(upload(allocs, &kp.cache_model, nullptr, cap * sizeof(int), stream));
     if (external_image) kp.image = ext_image;
     else PT_HIP(upload(allocs, &kp.image, nullptr, (size_t)npix_all * 3 * sizeof(float), stream));
-    kp.hs_pool_blocks = cfg.accel == ACCEL_GRID_FAST ? 65536 : 1;     // 64 MiB of 64-member blocks
+    {
+        const char* hpb = std::getenv("PT_HS_POOL_BLOCKS");          // 64-member blocks per pipeline
+        kp.hs_pool_blocks = cfg.accel == ACCEL_GRID_FAST ? (hpb ? std::max(1, std::atoi(hpb)) : 65536) : 1;   // 64 MiB
+    }
     {
         // Persistent trace + shading pass; PT_TRACE_SPLIT=0 / PT_GF_SPLIT=0 keep the fused kernel.
         const char* e = std::getenv("PT_TRACE_SPLIT");

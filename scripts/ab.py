@@ -63,19 +63,24 @@ def main():
         rs[v] = r
     times = {v: [] for v in a.variants}
     segs = {}
+    dfr = {v: 0 for v in a.variants}
     for rnd in range(a.rounds):
         for v, r in rs.items():
             s0 = r.segments()
+            d0 = r.deferred_rays()
             torch.cuda.synchronize()
             t = time.perf_counter()
             r.renderLoop(rnd * a.steps, a.steps)
             times[v].append((time.perf_counter() - t) / a.steps * 1e3)
             segs[v] = (r.segments() - s0) / a.steps
+            dfr[v] += r.deferred_rays() - d0
     out = {}
     for v in a.variants:
         med = statistics.median(times[v])
         out[v] = {"ms_per_spp_median": round(med, 3), "ms_min": round(min(times[v]), 3),
                   "Mrays_s": round(segs[v] / med / 1e3, 1)}
+        if dfr[v]:                                     # rays k_trace_deferred traced (hit-set pool exhausted / full)
+            out[v]["deferred_rays_per_spp"] = round(dfr[v] / (a.rounds * a.steps), 1)
         allc = rs[v].segments_per_bounce(159)
         if allc[71]:
             it = allc[71]
