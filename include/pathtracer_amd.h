@@ -64,7 +64,7 @@ typedef struct pt_render_config {
     double plane_z;           /* image plane z (Renderer.cpp:543), default 900 */
     double plane_x0, plane_y0, plane_w, plane_h;  /* Renderer.cpp:538-542: -10,-4,20,16 */
     int block;                /* bounce-kernel workgroup = compaction chunk: 64 (default), 128 or 256 */
-    int pipelines;            /* iterations in flight on their own HIP streams, 1..16 (default 16); results
+    int pipelines;            /* iterations in flight on their own HIP streams, 1..32 (default 16); results
                                  are identical for every value (contributions merge in iteration order).
                                  Loading the library sets GPU_MAX_HW_QUEUES=16 (one hardware queue per
                                  pipeline stream) unless the process already set it */
@@ -145,7 +145,7 @@ int pt_renderer_segments_per_bounce(pt_renderer *r, long long *out, int n);
 /* HIP-event timing read by kernel_stats: 0 off, 1 around every kernel group on every
  * pipeline, 2 around pipeline 0's trace phases only (light enough for a timed run). */
 int pt_renderer_set_profiling(pt_renderer *r, int on);
-/* Iterations in flight after allocate_on_gpu (config.pipelines clamped to 1..16, PT_PIPES overrides). */
+/* Iterations in flight after allocate_on_gpu (config.pipelines clamped to 1..32, PT_PIPES overrides). */
 int pt_renderer_pipelines(pt_renderer *r);
 /* stats[0..6] = secondary-bounce ms, scan ms, primary ms, secondary-bounce launches,
  * scan launches, first-bounce ms, first-bounce launches (HIP events; resets). */

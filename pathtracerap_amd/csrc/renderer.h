@@ -165,7 +165,7 @@ private:
 
     KParams kp{};                    // pipeline 0 (and everything the pipelines share)
     hipStream_t stream = nullptr;    // the caller's stream; pipeline 0 runs on it
-    static constexpr int kMaxPipes = 16;
+    static constexpr int kMaxPipes = 32;
     int npipes = 1;
     KParams pk[kMaxPipes]{};         // pipeline i's parameters (pk[0] == kp)
     hipStream_t pstream[kMaxPipes]{};    // pstream[0] == stream; 1.. created here

@@ -3070,7 +3070,9 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         kp.trace_refill = rf ? std::max(1, std::min(64, std::atoi(rf))) : (npipes > 1 ? 32 : 48);
         const char* rpl = std::getenv("PT_TRACE_RPL");
         // 4 rays per lane: +2.4 % at configs[4] (16 bounces, sparse late bounces), neutral at configs[1];
-        // off with one pipeline, where a launch has the chip to itself (its idle waves cost nothing)
+        // off with one pipeline, where a launch has the chip to itself (its idle waves cost nothing).
+        // Round 6: 8 for a BLAS beyond the aggregate L2 measured +2..3 % in-process but within noise as
+        // separate processes in steady state (1M +0.5 %, 10M 0; profiles/r06/ab_pipes_steady.txt): 4 stays
         kp.trace_rpl = rpl ? std::max(0, std::atoi(rpl)) : (npipes > 1 ? 4 : 0);
         const char* tf = std::getenv("PT_TRACE_FLAGS");
         kp.trace_flags = tf && bvh_split ? std::atoi(tf) : 11;
@@ -3116,8 +3118,11 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* wh = std::getenv("PT_WALK_HANDON");
         const char* wc = std::getenv("PT_WALK_WCAP");
         const bool handon = wh ? std::atoi(wh) != 0 : npipes > 1;
+        // Room: one record per lane of the launch, and at least one per 16 pixels -- a large frame
+        // hands on more walks per bounce than a launch has lanes (configs[2], 2800x2240: ~145k per
+        // bounce against 131k lanes sent 55k rays per sample to k_trace_deferred; -2.4 %).
         kp.cont_wcap = split_trace && cfg.accel == ACCEL_GRID_FAST && handon
-                           ? (wc ? std::max(0, std::atoi(wc)) : trace_blocks * 64) : 0;
+                           ? (wc ? std::max(0, std::atoi(wc)) : std::max(trace_blocks * 64, npix_all / 16)) : 0;
         const char* dl = std::getenv("PT_DRAIN_LEVELS");     // tail launches; the last one runs to the end
         kp.drain_levels = std::max(1, std::min(kDrainLevels, dl ? std::atoi(dl) : 1));
         kp.spill_stride = spills ? 2 * trace_blocks * 64 : 1;   // main lanes, then tail lanes' own areas

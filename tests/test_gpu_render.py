@@ -571,7 +571,7 @@ def test_allphase_iterations_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, m
 
 
 @pytest.mark.parametrize("accel", [1, 2])
-@pytest.mark.parametrize("rpl,minw", [("0", "2"), ("4", "2"), ("64", "1"), ("1000000", "1")])
+@pytest.mark.parametrize("rpl,minw", [("0", "2"), ("4", "2"), ("8", "2"), ("64", "1"), ("1000000", "1")])
 def test_main_launch_sized_to_the_rays_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, accel, rpl, minw):
     """PT_TRACE_RPL: a bounce whose rays come to fewer than rpl per lane runs only
     that many waves of its main trace launch (at least PT_TRACE_MIN_WAVES_PER_CU
@@ -622,3 +622,23 @@ def test_walk_handon_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypat
         assert deferred == 0, deferred
     else:
         assert deferred > 0
+
+
+def test_walk_handon_room_scales_with_the_frame(gpu, pt_mod):
+    """The walk hand-on records' room is at least one per 16 pixels, so a large
+    frame does not send rays to k_trace_deferred: the README scene at configs[2]'s
+    2800x2240 with 16 pipelines hands on ~2.3 % of a bounce's rays (~145k, more
+    than the launch's 131k lanes, the round-5 room; 55k rays per sample were then
+    deferred).  Results do not depend on the route (test_walk_handon_bit_identical);
+    this pins the route at the benched size."""
+    P = pt_mod
+    s = P.Scene(REF_SCENE)
+    s.build(bvh=True)
+    cfg = P.RenderConfig(width=2800, height=2240, iterations=2, max_bounces=5, accel=P.ACCEL_GRID_FAST, pipelines=16)
+    r = P.Renderer(cfg)
+    r.allocateOnGPU(s)
+    r.renderLoop()
+    deferred, faults = r.deferred_rays(), r.trace_faults()
+    r.free()
+    assert faults == 0
+    assert deferred == 0, deferred
