@@ -1749,9 +1749,6 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #ifndef PT_GF_TAIL_MINWAVES
 #define PT_GF_TAIL_MINWAVES 4 // the same for the tail launches (k_trace_gf<..., TAIL = true>)
 #endif
-#ifndef PT_HIT_LATE
-#define PT_HIT_LATE 0         // k_trace_gf: a finished ray's hit record stored behind the next claim (experiment)
-#endif
 #ifndef PT_LDS_TOP
 #define PT_LDS_TOP 0          // k_trace_gf: top 4-wide nodes per mesh staged in LDS (experiment; 0 = off)
 #endif
@@ -1938,8 +1935,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
     int cur = 0, sp = 0, nh = 0, tier = 0;
     int pblk = -1;                                  // global pool block holding the hit set (-1: LDS)
     int lf_i = 0, lf_e = 0, lf2_i = 0, lf2_e = 0, lf_next = -1;
-    constexpr bool kHitLate = PT_HIT_LATE != 0;
-    bool pend = false;                              // PT_HIT_LATE: this lane's finished ray's hit record not yet written
     int lbase = 0;                                  // ModelRec::leaf_base of the model being traced
     bool exhausted = false;
     unsigned cmask = 0;                            // PT_SEL_MASK: candidate models of the lane's ray
@@ -1960,11 +1955,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.cont_next + level - 1, cnt);
-            if (kHitLate && pend) {                                   // behind the claim
-                const int4 e = hs[0];
-                put_hit(p, e.w, __int_as_float(e.x), e.z, e.y);
-                pend = false;
-            }
             base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             if (base + cnt >= ncont) exhausted = true;
             if (state == 0) {
@@ -2033,11 +2023,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             const int leader = __ffsll((long long)idle) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(p.trace_next, cnt);
-            if (kHitLate && pend) {                                   // behind the claim
-                const int4 e = hs[0];
-                put_hit(p, e.w, __int_as_float(e.x), e.z, e.y);
-                pend = false;
-            }
             base = __builtin_amdgcn_readlane(base, leader);   // uniform: SGPR
             rstamp(0);
             if (base + cnt >= n) exhausted = true;
@@ -2140,11 +2125,7 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
                     im++;
                 }
                 if (im >= p.nmodels) {
-                    // PT_HIT_LATE: the hit record waits in the lane's (now unused) first hit-set slot
-                    // and is stored behind the next refill's claim, so that claim does not wait on
-                    // the record's store (vmcnt counts stores on gfx950)
-                    if (kHitLate) { hs[0] = make_int4(__float_as_int(gdist), gtri, gmodel, j); pend = true; }
-                    else put_hit(p, j, gdist, gmodel, gtri);
+                    put_hit(p, j, gdist, gmodel, gtri);
                     state = 0;
                     break;
                 }
@@ -2487,10 +2468,6 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             state = drain ? 3 : (state == 6 ? 0 : state);
         }
         if (stamps) { const unsigned long long t = clock64(); cy[5] += t - ts; ts = t; }
-    }
-    if (kHitLate && pend) {                         // lanes that finished after their wave's last claim
-        const int4 e = hs[0];
-        put_hit(p, e.w, __int_as_float(e.x), e.z, e.y);
     }
     if (stamps && lane == 0) {
         for (int q = 0; q < 6; q++) atomicAdd(p.segments + 20 + q + kMaxBounceCounters, cy[q]);
@@ -3092,6 +3069,8 @@ int Renderer::allocateOnGPU(const Scene& scene) {
         const char* wpc = std::getenv("PT_TRACE_WAVES_PER_CU");
         const int w = wpc ? std::max(1, std::atoi(wpc)) : (npipes > 1 ? 8 : 20);
         trace_blocks = std::max(1, cus) * w;
+        const char* tb = std::getenv("PT_TAIL_BLOCKS");
+        tail_blocks = tb ? std::max(1, std::min(trace_blocks, std::atoi(tb))) : trace_blocks;
         const char* mb = std::getenv("PT_TRACE_MIN_WAVES_PER_CU");
         kp.trace_min_blocks = std::max(1, cus) * (mb ? std::max(1, std::atoi(mb)) : 2);
         // k_trace_gf's 12-entry LDS stack; k_trace_bvh's 4-wide traversal (up to three pushes per node)
@@ -3171,6 +3150,10 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     if (!fork_ev) PT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     kp = pk[0];
     PT_HIP(hipStreamSynchronize(stream));
+    {
+        const char* fr = std::getenv("PT_FINAL_RPL");
+        final_rpl = fr && *fr >= '0' && *fr <= '9' ? std::max(0, std::atoi(fr)) : -1;
+    }
     const char* gr = std::getenv("PT_GRAPH");
     use_graph = gr && std::atoi(gr) != 0;
     allocated = true;
@@ -3264,11 +3247,14 @@ void Renderer::launchTrace(const KParams& k, hipStream_t st, int b) {
             else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 57>), g, t, 0, st, k, b, 0);
             else hipLaunchKernelGGL((k_trace_gf<64, 24>), g, t, 0, st, k, b, 0);
         }
+        // tail launches: PT_TAIL_BLOCKS workgroups (experiment; default the main launch's), each lane
+        // claiming records until they run out, so any grid traces every record
+        const dim3 gt((unsigned)tail_blocks);
         for (int l = 1; (k.drain_dump > 0 && l <= k.drain_levels) || (k.cont_wcap > 0 && l == 1); l++) {
             // the rays handed on (drain continuations; walk hand-ons go to level 1), packed
-            if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), g, t, 0, st, k, b, l);
-            else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 41, true>), g, t, 0, st, k, b, l);
-            else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), g, t, 0, st, k, b, l);
+            if (lds) hipLaunchKernelGGL((k_trace_gf<64, 9, true>), gt, t, 0, st, k, b, l);
+            else if (wide) hipLaunchKernelGGL((k_trace_gf<64, 41, true>), gt, t, 0, st, k, b, l);
+            else hipLaunchKernelGGL((k_trace_gf<64, 8, true>), gt, t, 0, st, k, b, l);
         }
         // normally empty (grid-stride over the deferred slots): a small grid keeps the empty launch short
         if (k.defer_launch)
@@ -3320,8 +3306,13 @@ void Renderer::launchBounce(const KParams& k, hipStream_t st, bool first, dim3 g
 
 // One iteration's bounce loop on pipeline q (stream st): sort / trace / shade /
 // scan per bounce.  iter = -1: k_bounce reads the id from k.iter_dev (capture).
-int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
-    const KParams& k = pk[q];
+int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes, bool last_wave) {
+    // The last wave of a renderLoop call (its final `pipelines` iterations) finishes with no other
+    // iterations left to fill the GPU: its sparse late bounces may size their trace launches for
+    // latency instead (PT_FINAL_RPL rays per lane; experiment).  Only the launch grids change.
+    KParams kl = pk[q];
+    if (last_wave && final_rpl >= 0) kl.trace_rpl = final_rpl;
+    const KParams& k = kl;
     const dim3 grid((unsigned)kp.nblocks + 8u);
     // profiling 1: an event pair around every kernel group on every pipeline; 2: around the
     // trace phases of pipeline 0 only (cheap enough for a timed region: 1/16 of the pairs)
@@ -3424,7 +3415,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
                 PT_HIP(ei);
             }
             PT_HIP(hipGraphLaunch(gexec[q], st));
-        } else if (enqueueIteration(q, st, iter, passes) != 0) {
+        } else if (enqueueIteration(q, st, iter, passes, n_iters - it <= np) != 0) {
             return -1;
         }
         if (np > 1) {
