@@ -158,7 +158,7 @@ private:
     int allocPipe(KParams& k, size_t cap, hipStream_t st);
     int fail(hipError_t e, const char* what);
     void freeBuffers();
-    int enqueueIteration(int q, hipStream_t st, int iter, int passes, bool last_wave = false);
+    int enqueueIteration(int q, hipStream_t st, int iter, int passes);
     void dropGraphs();
     int joinPipes(int np);
     int checkFaults();
@@ -185,7 +185,6 @@ private:
     bool split_trace = false;        // persistent k_trace_bvh / k_trace_gf + shading pass
     int trace_blocks = 0;
     int tail_blocks = 0;             // grid of k_trace_gf's tail launches (PT_TAIL_BLOCKS; default trace_blocks)
-    int final_rpl = -1;              // PT_FINAL_RPL: trace_rpl of a renderLoop call's last wave of iterations (-1: unchanged)
     int gf_flags = 9;                // k_trace_gf variant: 1 LDS model records, 8 phase scheduling
     bool gf_wide_lds = false;        // k_trace_gf default variants with 9..12 models: 12 LDS records (F | 32)
     bool bvh_wide_lds = false;       // k_trace_bvh default variant with 9..12 models: 12 LDS records (F = 43)

@@ -3150,10 +3150,6 @@ int Renderer::allocateOnGPU(const Scene& scene) {
     if (!fork_ev) PT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     kp = pk[0];
     PT_HIP(hipStreamSynchronize(stream));
-    {
-        const char* fr = std::getenv("PT_FINAL_RPL");
-        final_rpl = fr && *fr >= '0' && *fr <= '9' ? std::max(0, std::atoi(fr)) : -1;
-    }
     const char* gr = std::getenv("PT_GRAPH");
     use_graph = gr && std::atoi(gr) != 0;
     allocated = true;
@@ -3306,13 +3302,8 @@ void Renderer::launchBounce(const KParams& k, hipStream_t st, bool first, dim3 g
 
 // One iteration's bounce loop on pipeline q (stream st): sort / trace / shade /
 // scan per bounce.  iter = -1: k_bounce reads the id from k.iter_dev (capture).
-int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes, bool last_wave) {
-    // The last wave of a renderLoop call (its final `pipelines` iterations) finishes with no other
-    // iterations left to fill the GPU: its sparse late bounces may size their trace launches for
-    // latency instead (PT_FINAL_RPL rays per lane; experiment).  Only the launch grids change.
-    KParams kl = pk[q];
-    if (last_wave && final_rpl >= 0) kl.trace_rpl = final_rpl;
-    const KParams& k = kl;
+int Renderer::enqueueIteration(int q, hipStream_t st, int iter, int passes) {
+    const KParams& k = pk[q];
     const dim3 grid((unsigned)kp.nblocks + 8u);
     // profiling 1: an event pair around every kernel group on every pipeline; 2: around the
     // trace phases of pipeline 0 only (cheap enough for a timed region: 1/16 of the pairs)
@@ -3415,7 +3406,7 @@ int Renderer::renderLoop(int first_iter, int n_iters) {
                 PT_HIP(ei);
             }
             PT_HIP(hipGraphLaunch(gexec[q], st));
-        } else if (enqueueIteration(q, st, iter, passes, n_iters - it <= np) != 0) {
+        } else if (enqueueIteration(q, st, iter, passes) != 0) {
             return -1;
         }
         if (np > 1) {

@@ -106,3 +106,31 @@ def test_configs4_iteration_4095_bitexact(gpu, pt_mod, oracle_mod, scene_10m):
     assert seg == oseg
     assert_bitexact(img, oimg, "configs[4] id 4095")
     assert np.isfinite(img).all() and img.sum() > 0
+
+
+def test_configs1_full_frame_last_six_iterations_bitexact(gpu, pt_mod, oracle_mod, synth_dir):
+    """configs[1] at full size (1280x1024, 8 bounces, the default 16 pipelines):
+    ids 250..255, the last six of the 256-spp run, whole frame, against the
+    oracle's render of the same ids -- with test_configs1_bench_workload_bitexact
+    (ids 0-1) eight of the run's 256 iterations are pinned at full size."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=100_000))
+    s.build()
+    cfg = P.RenderConfig(width=1280, height=1024, iterations=6, max_bounces=8)
+    img, seg, oimg, oseg = _both(P, O, s, cfg, 250, 6)
+    assert seg == oseg
+    assert_bitexact(img, oimg, "configs[1] full frame ids 250-255")
+
+
+def test_target_1m_full_frame_last_iterations_bitexact(gpu, pt_mod, oracle_mod, synth_dir):
+    """north_star target (1M triangles) at full size: ids 1021..1023, the last
+    three of the 1024-spp run, whole frame."""
+    from pathtracerap_amd import synthetic
+    P, O = pt_mod, oracle_mod
+    s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=1_000_000))
+    s.build()
+    cfg = P.RenderConfig(width=1280, height=1024, iterations=3, max_bounces=8)
+    img, seg, oimg, oseg = _both(P, O, s, cfg, 1021, 3)
+    assert seg == oseg
+    assert_bitexact(img, oimg, "1M target full frame ids 1021-1023")

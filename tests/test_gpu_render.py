@@ -550,27 +550,23 @@ def test_tail_sized_to_records_bit_identical(gpu, pt_mod, oracle_mod, synth_dir,
     assert_bitexact(img, oimg, f"PT_TAIL_RPL={rpl} PT_TAIL_REFILL={refill} levels={levels}")
 
 
-@pytest.mark.parametrize("blocks,levels,final_rpl", [("1", "1", "X"), ("7", "2", "X"), ("512", "1", "0"),
-                                                    ("1", "1", "1")])
-def test_tail_grid_and_final_wave_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, blocks, levels,
-                                                final_rpl):
+@pytest.mark.parametrize("blocks,levels", [("1", "1"), ("7", "2"), ("512", "1")])
+def test_tail_grid_bit_identical(gpu, pt_mod, oracle_mod, synth_dir, monkeypatch, blocks, levels):
     """PT_TAIL_BLOCKS: k_trace_gf's tail launches run on a grid of that many
     workgroups, whose lanes claim drained / walk hand-on records until none is
-    left (one workgroup resumes them all); PT_FINAL_RPL: the last wave of
-    iterations sizes its main trace launches differently.  Only which lane
-    traces which ray changes: images and segment counts stay the oracle's."""
+    left (one workgroup resumes them all).  Only which lane traces which ray
+    changes: images and segment counts stay the oracle's."""
     from pathtracerap_amd import synthetic
     P, O = pt_mod, oracle_mod
     monkeypatch.setenv("PT_DRAIN_DUMP", "24")
     monkeypatch.setenv("PT_DRAIN_LEVELS", levels)
     monkeypatch.setenv("PT_TAIL_BLOCKS", blocks)
-    monkeypatch.setenv("PT_FINAL_RPL", final_rpl)
     s = P.Scene(synthetic.diffuse_scene(synth_dir, ntri=6000, seed=13, metallic=True))
     s.build(bvh=True)
     cfg = P.RenderConfig(width=211, height=97, iterations=5, max_bounces=7, accel=P.ACCEL_GRID_FAST, pipelines=4)
     img, seg, oimg, oseg = _render_both(P, O, s, cfg)
     assert seg == oseg
-    assert_bitexact(img, oimg, f"PT_TAIL_BLOCKS={blocks} levels={levels} PT_FINAL_RPL={final_rpl}")
+    assert_bitexact(img, oimg, f"PT_TAIL_BLOCKS={blocks} levels={levels}")
 
 
 @pytest.mark.parametrize("lanes,pipes", [("16", 4), ("64", 4), ("64", 1)])
