@@ -56,7 +56,8 @@ def test_reference_scene_bvh(pt_mod):
     s.build(bvh=True)
     b = s.export_bvh()
     c = s.counts()
-    assert c["nbvh_refs"] == c["nt"]
+    # every triangle once; 64-byte leaf records (PT_TRI_REC 4) add padding slots (triangle -1)
+    assert (b["refs"] >= 0).sum() == c["nt"] and c["nbvh_refs"] >= c["nt"]
     for r in b["roots"]:
         _, depth = _walk(b["nodes"], r)
         assert depth <= 23
