@@ -66,9 +66,6 @@ struct Builder {
     Child leaf(int b, int e, const Box& box) {
         Child c;
         c.box = box;
-        // 64-byte records: a leaf of two or more triangles starts at an even slot (one 128-byte line
-        // for two); the skipped slot is padding (triangle -1, in no leaf)
-        if (kTriRec == 4 && e - b >= 2 && (s.bvh_tri_order.size() & 1)) s.bvh_tri_order.push_back(-1);
         c.link = (int)s.bvh_tri_order.size();
         c.count = e - b;
         for (int i = b; i < e; i++) s.bvh_tri_order.push_back(refs[i].tri);

@@ -5,17 +5,6 @@
 
 namespace pt {
 
-// Leaf triangle records (Scene::bvh_tri_geom): PT_TRI_REC float4 per leaf slot -- 3: v0, e1, e2 with the
-// triangle index and packed voxel box in the w lanes (48 bytes); 4: the same plus a pad float4 (64 bytes),
-// and every leaf of two or more triangles starts at an even slot, so a two-triangle leaf is exactly one
-// 128-byte line (with 48-byte records 5 of 8 such leaves straddle two lines).  Padding slots hold
-// triangle -1 and belong to no leaf.
-#ifndef PT_TRI_REC
-#define PT_TRI_REC 3
-#endif
-constexpr int kTriRec = PT_TRI_REC;
-static_assert(kTriRec == 3 || kTriRec == 4, "PT_TRI_REC: 3 or 4 float4 per leaf triangle record");
-
 // Primitive.h:109-114 SpatialAcceleration::EntityType
 enum EntityType : int { ENTITY_MODEL = 0, ENTITY_SCENE = 1, ENTITY_TRIANGLE = 2, ENTITY_SPHERE = 3 };
 

@@ -314,7 +314,7 @@ __device__ bool bvh_closest(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 
     unsigned n_nodes = 0, n_tris = 0;   // PT_DEBUG_ABLATE & 8 statistics
     auto leaf = [&](int first, int count) {
         for (int i = first; i < first + count; i++) {
-            const float4 A = p.bvh_tri_geom[kTriRec * i], B = p.bvh_tri_geom[kTriRec * i + 1], C = p.bvh_tri_geom[kTriRec * i + 2];
+            const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
             const int it = __float_as_int(A.w);
             float t;
             n_tris++;
@@ -351,7 +351,7 @@ __device__ int bvh_collect(const KParams& p, const ModelRec& M, f3 o, f3 d, f3 n
     unsigned nvis = 0;
     auto leaf = [&](int first, int count) {
         for (int i = first; i < first + count; i++) {
-            const float4 A = p.bvh_tri_geom[kTriRec * i], B = p.bvh_tri_geom[kTriRec * i + 1], C = p.bvh_tri_geom[kTriRec * i + 2];
+            const float4 A = p.bvh_tri_geom[3 * i], B = p.bvh_tri_geom[3 * i + 1], C = p.bvh_tri_geom[3 * i + 2];
             float t;
             if (!tri_test_rec(A, B, C, o, d, t)) continue;
             if (BOUNDED) {
@@ -1606,7 +1606,7 @@ __global__ __launch_bounds__(BS, PT_BVH_MINWAVES) void k_trace_bvh(KParams p, in
 #pragma unroll
             for (int q = 0; q < PT_LEAF_STEP; q++) {
                 const int iq = lf_i + q < lf_e ? lf_i + q : lf_i;
-                TA[q] = p.bvh_tri_geom[kTriRec * iq]; TB[q] = p.bvh_tri_geom[kTriRec * iq + 1]; TC[q] = p.bvh_tri_geom[kTriRec * iq + 2];
+                TA[q] = p.bvh_tri_geom[3 * iq]; TB[q] = p.bvh_tri_geom[3 * iq + 1]; TC[q] = p.bvh_tri_geom[3 * iq + 2];
             }
 #pragma unroll
             for (int q = 0; q < PT_LEAF_STEP; q++) {
@@ -2166,8 +2166,8 @@ __global__ __launch_bounds__(BS, TAIL ? PT_GF_TAIL_MINWAVES : PT_GF_MINWAVES) vo
             // per step, their loads issued together; tested in leaf order, as one per step would
             // (k_trace_gf: at most two -- selecting from a longer array spilled 33+ VGPRs)
             const int i1 = (PT_LEAF_STEP > 1 && lf_i + 1 < lf_e) ? lf_i + 1 : lf_i;
-            const float4 A0 = p.bvh_tri_geom[kTriRec * lf_i], B0 = p.bvh_tri_geom[kTriRec * lf_i + 1], C0 = p.bvh_tri_geom[kTriRec * lf_i + 2];
-            const float4 A1 = p.bvh_tri_geom[kTriRec * i1], B1 = p.bvh_tri_geom[kTriRec * i1 + 1], C1 = p.bvh_tri_geom[kTriRec * i1 + 2];
+            const float4 A0 = p.bvh_tri_geom[3 * lf_i], B0 = p.bvh_tri_geom[3 * lf_i + 1], C0 = p.bvh_tri_geom[3 * lf_i + 2];
+            const float4 A1 = p.bvh_tri_geom[3 * i1], B1 = p.bvh_tri_geom[3 * i1 + 1], C1 = p.bvh_tri_geom[3 * i1 + 2];
             const int n_step = i1 != lf_i ? 2 : 1;
             if (PT_TRACE_STATS && (p.debug & 16)) atomicAdd(p.segments + 68 + kMaxBounceCounters, (unsigned long long)n_step);
             // Both tests first (pure), then the hits' insertions in leaf order: the loop

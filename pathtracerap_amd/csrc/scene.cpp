@@ -571,18 +571,13 @@ void Scene::buildDeviceTables() {
         float* q = &tri_normal[t * 4];
         q[0] = n.x; q[1] = n.y; q[2] = n.z; q[3] = 0.0f;
     }
-    constexpr size_t R = 4 * kTriRec;                 // floats per leaf slot (pt_types.h)
-    bvh_tri_geom.assign(bvh_tri_order.size() * R, 0.0f);
+    bvh_tri_geom.assign(bvh_tri_order.size() * 12, 0.0f);
     for (size_t i = 0; i < bvh_tri_order.size(); i++) {
         const int t = bvh_tri_order[i];
-        if (t < 0) {                                  // padding slot (PT_TRI_REC 4): in no leaf
-            std::memcpy(&bvh_tri_geom[i * R + 3], &t, sizeof(int));
-            continue;
-        }
-        std::memcpy(&bvh_tri_geom[i * R], &tri_geom[(size_t)t * 12], 12 * sizeof(float));
-        std::memcpy(&bvh_tri_geom[i * R + 3], &t, sizeof(int));
-        std::memcpy(&bvh_tri_geom[i * R + 7], &tri_vbox[2 * (size_t)t], sizeof(int));
-        std::memcpy(&bvh_tri_geom[i * R + 11], &tri_vbox[2 * (size_t)t + 1], sizeof(int));
+        std::memcpy(&bvh_tri_geom[i * 12], &tri_geom[(size_t)t * 12], 12 * sizeof(float));
+        std::memcpy(&bvh_tri_geom[i * 12 + 3], &t, sizeof(int));
+        std::memcpy(&bvh_tri_geom[i * 12 + 7], &tri_vbox[2 * (size_t)t], sizeof(int));
+        std::memcpy(&bvh_tri_geom[i * 12 + 11], &tri_vbox[2 * (size_t)t + 1], sizeof(int));
     }
     model_recs.resize(models.size());
     model_shade.resize(models.size());
