@@ -768,8 +768,8 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
 
 // Fast walk certificate: a cheaper sufficient condition for the common case,
 // tried before walk_certify.  It decides the walk's result as (t_min, m*) when
-// m* is the UNIQUE minimum-t member and the walk provably tests it before it
-// can stop.  The lemma both certificates rest on: at every walk parameter s
+// m* is the unique minimum-t member (or every minimum-t member has m*'s voxel
+// box, index = their lowest) and the walk provably tests it before it can stop.  The lemma both certificates rest on: at every walk parameter s
 // (from pt) the walk's voxel holds, per axis a, a point within
 // delta_a = cslack_a + |d_a| errm of the exact ray point ray(s) (the DDA's
 // +EPSILON start shift and its crossing-parameter rounding, errm bounding the
@@ -785,25 +785,34 @@ __device__ __forceinline__ bool walk_certify(const KParams& p, const ModelRec& M
 //      whole box stands in for it.  g_h > s* (or a grown box the ray misses, or
 //      a start inside B*, whose start voxel then is m*'s) means no voxel before
 //      the walk reaches m*'s box is a hit voxel: the walk cannot stop before
-//      testing m*, and m*'s unique minimum t makes the result (t_min, m*).
+//      testing m*, and m*'s minimum t makes the result (t_min, m*) (tied members
+//      of m*'s box are tested in the same voxel: the lowest index wins).
 // (iii) The voxel holding s* was entered at a parameter <= s*: within the
 //      window when t_box + s* < t_min + win (plus rounding slack).
-// Any doubt (ties at t_min, zero slopes, boxes too thin to shrink, rays that
-// only graze B*) returns false and walk_certify / the exact walk decide.
+// Any doubt (ties at t_min among different boxes, zero slopes, boxes too thin
+// to shrink, rays that only graze B*) returns false and walk_certify / the
+// exact walk decide.
 template <int CAP, class GetM>
 __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelRec& M, f3 d, f3 inv, f3 pt, float t_box,
                                                   GetM get, int nh, float tmin, float win, int& tri) {
+    // m*: the minimum-t member, or several tied at t_min whose voxel boxes are identical (the two
+    // triangles of a quad split along its diagonal share their box: 72 % of the fast certificate's
+    // failures at configs[1] were such ties).  Tied members with one box B* are all tested in the
+    // walk's first voxel of B*, where the lowest index among them wins (walk_step_g's (t, step,
+    // index) order), so they act as one member with that index.
     int cnt = 0;
-    int ms_y = 0, ms_z = 0, ms_w = 0;              // m*'s index and packed voxel box (per component:
-#pragma unroll                                     // a select of whole int4s went through scratch memory)
+    bool same = true;                               // every minimum-t member has m*'s box
+    int ms_y = 0x7fffffff, ms_z = 0, ms_w = 0;      // m*'s index and packed voxel box (per component:
+#pragma unroll                                      // a select of whole int4s went through scratch memory)
     for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
         if (CAP > 0 && h >= nh) break;
         const int4 e = get(h);
         const bool mn = __int_as_float(e.x) == tmin;
+        same = same & (!mn | (cnt == 0) | ((e.z == ms_z) & (e.w == ms_w)));
+        ms_z = (mn & (cnt == 0)) ? e.z : ms_z;
+        ms_w = (mn & (cnt == 0)) ? e.w : ms_w;
+        ms_y = mn ? min(ms_y, e.y) : ms_y;
         cnt += mn ? 1 : 0;
-        ms_y = mn ? e.y : ms_y;
-        ms_z = mn ? e.z : ms_z;
-        ms_w = mn ? e.w : ms_w;
     }
     const float pp[3] = {pt.x, pt.y, pt.z}, dv[3] = {d.x, d.y, d.z}, iv[3] = {inv.x, inv.y, inv.z};
     int bl[3], bh[3];
@@ -841,11 +850,12 @@ __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelR
     }
     const float sl = 1e-5f * (absr(x) + 1.0f);
     const float ss = fmaxf(e, 0.0f) + sl;
-    bool ok = (cnt == 1) & (dv[0] != 0.0f) & (dv[1] != 0.0f) & (dv[2] != 0.0f) & thick & (sB <= xB) &
+    bool ok = (cnt >= 1) & same & (dv[0] != 0.0f) & (dv[1] != 0.0f) & (dv[2] != 0.0f) & thick & (sB <= xB) &
               (ss + sl < x) & (absr(x) < 1e30f) & (errm < 1e30f);
     const float tw = t_box + ss;
     ok = ok & (tw + 1e-5f * (absr(tw) + 1.0f) < tmin + win);
     const bool start_in = e < 0.0f;               // the walk's start voxel is m*'s
+    bool mfail1 = false, mfailn = false;          // stats build: a member failed with one / several extensions
 #pragma unroll
     for (int h = 0; h < (CAP > 0 ? CAP : nh); h++) {
         if (CAP > 0 && h >= nh) break;
@@ -886,7 +896,21 @@ __device__ __forceinline__ bool walk_certify_fast(const KParams& p, const ModelR
             const bool missed = (g > go + 1e-5f * (absr(go) + 1.0f)) & (absr(g) < 1e30f);
             const bool after = (g - 1e-5f * (absr(g) + 1.0f) > ss) & (absr(g) < 1e30f);
             ok = ok & (missed | after);
+            if (PT_TRACE_STATS) {
+                mfail1 = mfail1 | (!(missed | after) & (ext == 1));
+                mfailn = mfailn | (!(missed | after) & (ext > 1));
+            }
         }
+    }
+    if (PT_TRACE_STATS && (p.debug & 4) && !ok) {   // the first failed condition (slots 80..87)
+        const int r = !((cnt >= 1) & same) ? 0
+                    : !((dv[0] != 0.0f) & (dv[1] != 0.0f) & (dv[2] != 0.0f)) ? 1
+                    : !thick ? 2
+                    : !(sB <= xB) ? 3
+                    : !((ss + sl < x) & (absr(x) < 1e30f) & (errm < 1e30f)) ? 4
+                    : !(tw + 1e-5f * (absr(tw) + 1.0f) < tmin + win) ? 5
+                    : mfail1 ? 6 : mfailn ? 7 : 5;
+        atomicAdd(p.segments + 80 + r + kMaxBounceCounters, 1ull);
     }
     tri = ms_y;
     return ok;

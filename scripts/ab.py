@@ -140,6 +140,11 @@ def main():
         if allc[86]:
             out[v]["collect_nodes_per_collection"] = round(allc[85] / allc[86], 2)
             out[v]["collections_per_segment"] = round(allc[86] / rs[v].segments(), 3)
+        if any(allc[143:151]):                         # slots 80..87: the fast certificate's first failed condition
+            tot = max(sum(allc[143:151]), 1)
+            out[v]["cert_fast_fail_share"] = dict(zip(
+                ["ties_or_none", "zero_dir", "thin_box", "misses_Bstar", "grazes_Bstar", "window",
+                 "member_one_extension", "member_several_extensions"], [round(c / tot, 4) for c in allc[143:151]]))
         if allc[105]:                                  # slots 40..42: fast / full certificate outcomes
             out[v]["cert_attempts_per_segment"] = round(allc[105] / max(rs[v].segments(), 1), 5)
             out[v]["cert_fast_ok_share"] = round(allc[103] / allc[105], 4)
