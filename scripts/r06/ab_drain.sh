@@ -1,0 +1,16 @@
+# Drain threshold (PT_DRAIN_DUMP: a main-launch wave hands its rays to the tail once at most this many
+# lanes still trace after the claims run out; default 16) at the final code: separate bench.py processes,
+# interleaved rounds, configs[1] at 20 and 64 timed iterations and 10M at 32.
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out &&
+B="--no-cpu-baseline --no-profile --alt-accel= --targets= --no-full-runs --warmup 5"
+run() {   # label, env, args
+  env $2 timeout -k 10 300 python bench.py $B $3 > gpurun_out/dr.json 2> gpurun_out/dr.err || { tail -5 gpurun_out/dr.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/dr.json')); print('$1', d['value'], d['ms_per_step'], d['config']['trace_faults'])" | tee -a gpurun_out/drain_rounds.txt
+}
+for r in 1 2; do
+  for v in 16 12 24 32; do
+    run "r$r 100k s20 dump=$v" "PT_DRAIN_DUMP=$v" "--steps 20"
+    run "r$r 100k s64 dump=$v" "PT_DRAIN_DUMP=$v" "--steps 64"
+    run "r$r 10M s32 dump=$v" "PT_DRAIN_DUMP=$v" "--ntri 10000000 --bounces 16 --inmem --steps 32"
+  done
+done
